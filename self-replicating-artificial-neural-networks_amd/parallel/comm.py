@@ -1,0 +1,171 @@
+"""SPMD communication layer (replaces the external ``distributed_computing`` job pool).
+
+One process per GPU, launched by ``torch.distributed.run`` (or the CLI's ``--nproc`` spawner).
+The control plane (generation table, RNG, selection) is *replicated* on every rank; the data plane
+(training a shard of organisms) is sharded.  Per generation there is exactly one packed
+all-gather of fixed-width records (M3) -- metrics + bit-packed offspring genotypes -- instead of
+the reference's pickled pandas objects over TCP.
+
+* GPU: backend ``nccl`` (= RCCL over xGMI on ROCm), payload tensors live on the local GPU.
+* CPU: backend ``gloo`` (tests, world_size > 1 emulation).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from datetime import timedelta
+from typing import Any, List, Optional
+
+import numpy as np
+
+
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self):
+        pass
+
+    def allgather_bytes(self, payload: bytes) -> List[bytes]:
+        return [payload]
+
+    def broadcast_bytes(self, payload: Optional[bytes], src: int = 0) -> bytes:
+        return payload
+
+    def allgather_object(self, obj: Any) -> List[Any]:
+        return [pickle.loads(b) for b in self.allgather_bytes(pickle.dumps(obj))]
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        b = self.broadcast_bytes(pickle.dumps(obj) if self.rank == src else None, src)
+        return pickle.loads(b)
+
+    def allreduce_max(self, value: float) -> float:
+        return value
+
+    def shutdown(self):
+        pass
+
+
+class LocalComm(Comm):
+    """world_size == 1."""
+
+
+class TorchDistComm(Comm):
+    """torch.distributed communicator.  Uses byte tensors so that one all-gather moves all
+    of a rank's results; on RCCL the tensors are device tensors (no host staging in RCCL)."""
+
+    def __init__(self, backend: Optional[str] = None, device=None, timeout_s: int = 1800):
+        import torch
+        import torch.distributed as dist
+        self.dist = dist
+        self.torch = torch
+        if not dist.is_initialized():
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            dist.init_process_group(backend=backend, timeout=timedelta(seconds=timeout_s))
+        self.backend = dist.get_backend()
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+        self.local_rank = int(os.environ.get("LOCAL_RANK", self.rank))
+        if device is None:
+            device = torch.device("cuda", self.local_rank) if self.backend == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+
+    def barrier(self):
+        if self.backend == "nccl":
+            self.dist.barrier(device_ids=[self.device.index])
+        else:
+            self.dist.barrier()
+
+    def _tensor(self, payload: bytes):
+        t = self.torch.frombuffer(bytearray(payload), dtype=self.torch.uint8) if payload else \
+            self.torch.zeros(0, dtype=self.torch.uint8)
+        return t.to(self.device)
+
+    def allgather_bytes(self, payload: bytes) -> List[bytes]:
+        torch = self.torch
+        n = torch.tensor([len(payload)], dtype=torch.int64, device=self.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world_size)]
+        self.dist.all_gather(sizes, n)
+        sizes = [int(s.item()) for s in sizes]
+        mx = max(sizes)
+        buf = torch.zeros(mx, dtype=torch.uint8, device=self.device)
+        if payload:
+            buf[:len(payload)] = self._tensor(payload)
+        out = torch.empty(self.world_size * mx, dtype=torch.uint8, device=self.device)
+        self.dist.all_gather_into_tensor(out, buf)
+        host = out.cpu().numpy()
+        return [host[r * mx:r * mx + sizes[r]].tobytes() for r in range(self.world_size)]
+
+    def broadcast_bytes(self, payload: Optional[bytes], src: int = 0) -> bytes:
+        torch = self.torch
+        n = torch.tensor([len(payload) if self.rank == src else 0], dtype=torch.int64, device=self.device)
+        self.dist.broadcast(n, src)
+        size = int(n.item())
+        buf = self._tensor(payload) if self.rank == src else torch.empty(size, dtype=torch.uint8,
+                                                                          device=self.device)
+        if size:
+            self.dist.broadcast(buf, src)
+        return buf.cpu().numpy().tobytes()
+
+    def allreduce_max(self, value: float) -> float:
+        t = self.torch.tensor([float(value)], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def shutdown(self):
+        if self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def make_comm(distributed: Optional[bool] = None, backend: Optional[str] = None) -> Comm:
+    """Create the communicator from the environment (``WORLD_SIZE`` set by torchrun)."""
+    if distributed is None:
+        distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if not distributed:
+        return LocalComm()
+    return TorchDistComm(backend=backend)
+
+
+# ------------------------------------------------------------------------------------------------
+# fixed-width result records (M3): metrics + bit-packed offspring pools
+# ------------------------------------------------------------------------------------------------
+METRIC_FIELDS = ("classification_validation_accuracy", "classification_training_accuracy",
+                 "classification_test_accuracy", "replication_mse")
+
+
+def pack_results(indices: np.ndarray, metrics: np.ndarray, offspring: np.ndarray,
+                 learning_time: float, replication_time: float) -> bytes:
+    """indices: (n,) int32 organism indices in the generation table; metrics: (n, 4) float64;
+    offspring: (n, pool, L) {0,1} -> bit-packed."""
+    n = len(indices)
+    header = np.array([n, offspring.shape[1] if n else 0, offspring.shape[2] if n else 0],
+                      dtype=np.int64).tobytes()
+    times = np.array([learning_time, replication_time], dtype=np.float64).tobytes()
+    body = np.asarray(indices, np.int32).tobytes() + np.asarray(metrics, np.float64).tobytes()
+    bits = np.packbits(np.asarray(offspring, np.uint8), axis=-1).tobytes() if n else b""
+    return header + times + body + bits
+
+
+def unpack_results(payload: bytes):
+    n, pool, L = np.frombuffer(payload[:24], dtype=np.int64)
+    lt, rt = np.frombuffer(payload[24:40], dtype=np.float64)
+    off = 40
+    idx = np.frombuffer(payload[off:off + 4 * n], dtype=np.int32)
+    off += 4 * n
+    metrics = np.frombuffer(payload[off:off + 8 * n * 4], dtype=np.float64).reshape(n, 4)
+    off += 8 * n * 4
+    if n:
+        nbytes = (L + 7) // 8
+        bits = np.frombuffer(payload[off:off + n * pool * nbytes], dtype=np.uint8).reshape(n, pool, nbytes)
+        offspring = np.unpackbits(bits, axis=-1)[..., :L]
+    else:
+        offspring = np.zeros((0, 0, 0), np.uint8)
+    return idx, metrics, offspring, float(lt), float(rt)

@@ -1,0 +1,32 @@
+"""Loader for the in-tree native extensions (built by ``__graft_entry__.build`` /
+``python -m serann.build``).  Extensions live in ``serann/_native`` so they travel with the repo
+snapshot; nothing is installed into site-packages."""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sysconfig
+from pathlib import Path
+
+NATIVE_DIR = Path(__file__).resolve().parent.parent / "_native"
+_cache = {}
+
+
+def load(name: str, required: bool = False):
+    """Import ``serann/_native/<name><EXT_SUFFIX>``; returns None (or raises) if absent."""
+    if name in _cache:
+        return _cache[name]
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    path = NATIVE_DIR / f"{name}{suffix}"
+    mod = None
+    if path.exists():
+        if name.startswith("serann_hip"):
+            import torch  # noqa: F401  -- HIP runtime must come from torch's bundled libamdhip64
+        spec = importlib.util.spec_from_file_location(name, str(path))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    elif required:
+        raise ImportError(f"native extension {name} not built (expected {path}); "
+                          f"run `python -c 'import __graft_entry__ as g; g.build()'`")
+    _cache[name] = mod
+    return mod
