@@ -1,0 +1,120 @@
+#!/usr/bin/env python
+"""Headline benchmark: SeRANN generations at pop = 125 x N GPUs (pop = 1000 at 8 GPUs).
+
+BASELINE.json metric: "seconds/generation at pop=1000 (8 GPUs) + SeRANN trained/sec at 1/2/4/8 GPUs".
+One *step* is one full generation of the full_experiment.json config: decode, train every organism
+5 epochs x 76 steps (batch 750, Keras Adam), validation each epoch, test evaluation, replication,
+fertility, multinomial offspring counts, selection + proofreading, decode, population statistics and
+the SQLite writes.  Per-GPU work is fixed as N grows (125 organisms per GPU) -> weak scaling.
+
+Data is synthetic (no network): MNIST-shaped learnable images, random genotype encodings, random-init
+weights, and the synthetic table codec that decodes genotypes into architectures drawn from the
+reference generator distribution.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+import uuid
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_SERANN_PER_SEC = 0.40   # pop=50, ~126 s/generation on 1x Titan X (3.5 h / 100 gens)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pop-per-gpu", type=int, default=125)
+    ap.add_argument("--engine", default="auto")
+    ap.add_argument("--parameters", default=None)
+    ap.add_argument("--profile-dir", default=None)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from serann.config import default_parameters, load_parameters
+    from serann.experiment.experiment import Experiment
+    from serann.experiment.runner import setup
+    from serann.parallel.comm import make_comm
+    from serann.utils.db import ExperimentDB
+
+    comm = make_comm()
+    params = load_parameters(args.parameters) if args.parameters else default_parameters("full_experiment")
+    pop = args.pop_per_gpu * comm.world_size
+    params["num_seranns"] = pop
+    params["num_generations"] = args.warmup + args.steps
+    s = setup(params, engine=args.engine, comm=comm)
+    is_cuda = s.device.startswith("cuda")
+
+    db = None
+    tmpdir = tempfile.mkdtemp(prefix="serann_bench_")
+    if comm.is_root:
+        db = ExperimentDB(os.path.join(tmpdir, f"{uuid.uuid4()}.sqlite"))
+    exp = Experiment("bench", s.encodings, s.worker, db, params, s.codec, comm=comm, random_seed=79375,
+                     verbose=bool(os.environ.get("SERANN_VERBOSE")))
+
+    marks = {}
+
+    def on_generation(gen, rec):
+        if gen == args.warmup - 1:
+            if is_cuda:
+                torch.cuda.synchronize()
+            comm.barrier()
+            marks["t0"] = time.perf_counter()
+        if comm.is_root:
+            print(json.dumps({"progress": rec}), file=sys.stderr, flush=True)
+
+    if args.warmup == 0:
+        comm.barrier()
+        marks["t0"] = time.perf_counter()
+    hist = exp.execute(on_generation=on_generation)
+    if is_cuda:
+        torch.cuda.synchronize()
+    comm.barrier()
+    t1 = time.perf_counter()
+    timed = [h for h in hist if h["generation"] >= args.warmup]
+    k = len(timed)
+    elapsed = t1 - marks.get("t0", t1)
+    elapsed = comm.allreduce_max(elapsed)
+    if comm.is_root:
+        sec_per_gen = elapsed / max(k, 1)
+        value = pop * k / elapsed if elapsed > 0 and k else 0.0
+        out = {
+            "metric": "serann_trained_per_sec",
+            "value": value,
+            "unit": "SeRANN/s (population organisms processed per second, whole job)",
+            "n_gpus": comm.world_size,
+            "steps": k,
+            "warmup": args.warmup,
+            "ms_per_step": sec_per_gen * 1000.0,
+            "seconds_per_generation": sec_per_gen,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / BASELINE_SERANN_PER_SEC,
+            "dtype": "bf16",
+            "data": "synthetic (MNIST-shaped images, random genotype encodings, table codec over "
+                    "generator-sampled architectures, random-init weights)",
+            "engine": s.engine,
+            "config": {"model": "SeRANN population, full_experiment.json (5 epochs, batch 750, "
+                                "architectures from the reference generator distribution)",
+                       "global_batch": int(params["training_batch_size"]), "seq_len": int(params["genotype_size"]),
+                       "population": pop, "parallelism": f"population-sharded dp{comm.world_size}"},
+            "generations": timed,
+        }
+        print(json.dumps(out), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

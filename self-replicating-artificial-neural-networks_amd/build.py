@@ -1,0 +1,91 @@
+"""Build the in-tree native extensions.
+
+* ``serann_host`` -- C++17 host runtime (Levenshtein, genotype statistics), g++.
+* ``serann_hip``  -- HIP/CDNA4 kernels for gfx950, hipcc ``--offload-arch=gfx950`` (cross-compiles
+  without a GPU).  Written directly for CDNA4: no hipify, no CUDA shims.
+
+Both land in ``serann/_native`` (git-ignored, but shipped with the repo snapshot).
+
+    python -m serann.build [--only host|hip] [--jobs N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+NATIVE = PKG / "_native"
+CSRC = PKG / "csrc"
+OFFLOAD_ARCH = os.environ.get("SERANN_OFFLOAD_ARCH", "gfx950")
+
+
+def _pybind_includes():
+    import pybind11
+    return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _ext_suffix():
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def build_host():
+    NATIVE.mkdir(exist_ok=True)
+    out = NATIVE / f"serann_host{_ext_suffix()}"
+    _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", *_pybind_includes(),
+          str(CSRC / "host" / "serann_host.cpp"), "-o", str(out)])
+    return out
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise FileNotFoundError("hipcc not found")
+
+
+def build_hip(jobs: int = 4):
+    NATIVE.mkdir(exist_ok=True)
+    build_dir = PKG / "_build"
+    build_dir.mkdir(exist_ok=True)
+    hipcc = _hipcc()
+    srcs = sorted((CSRC / "hip").glob("*.hip"))
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", "-mcode-object-version=5",
+             "-Wno-unused-result", f"-I{CSRC / 'hip'}", *_pybind_includes()]
+    objs = []
+
+    def compile_one(src):
+        obj = build_dir / (src.stem + ".o")
+        _run([hipcc, *flags, "-c", str(src), "-o", str(obj)])
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    out = NATIVE / f"serann_hip{_ext_suffix()}"
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", *map(str, objs), "-o", str(out)])
+    return out
+
+
+def build_all(jobs: int = 4):
+    return [build_host(), build_hip(jobs)]
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", choices=["host", "hip"], default=None)
+    ap.add_argument("--jobs", type=int, default=4)
+    a = ap.parse_args()
+    if a.only in (None, "host"):
+        build_host()
+    if a.only in (None, "hip"):
+        build_hip(a.jobs)

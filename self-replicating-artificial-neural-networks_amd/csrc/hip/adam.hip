@@ -1,0 +1,82 @@
+// Fused multi-tensor Keras-Adam over a flat fp32 parameter arena (K13 / K38).
+//
+// TF ResourceApplyAdam semantics (experiment_worker.py:80): lr_t = lr*sqrt(1-b2^t)/(1-b1^t),
+// m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr_t m / (sqrt(v) + eps).
+// One launch per training step for the whole population shard; the step counter and lr_t live in
+// device memory so the launch can be captured once in a hipGraph and replayed every step.  The
+// kernel also refreshes the bf16 compute copy of the weights and zeroes the gradient arena for the
+// next step's split-K / atomic accumulation.  Pure HBM streaming: 4x float4 in, 4x float4 + bf16 out.
+#include "common.h"
+#include "serann_hip.h"
+
+__global__ void adam_scalars_kernel(int* step, float* lr_t, float lr, float b1, float b2) {
+    int t = *step + 1;
+    *step = t;
+    *lr_t = lr * sqrtf(1.f - powf(b2, (float)t)) / (1.f - powf(b1, (float)t));
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ pbf, const float* __restrict__ lr_t_ptr,
+                                                   int64_t n, float b1, float b2, float eps) {
+    const float lr_t = *lr_t_ptr;
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pv = reinterpret_cast<float4*>(p)[i];
+        float4 gv = reinterpret_cast<float4*>(g)[i];
+        float4 mv = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        float* pp = &pv.x; float* gg = &gv.x; float* mm = &mv.x; float* vvv = &vv.x;
+        ushort4 ob;
+        uint16_t* o = &ob.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
+            vvv[k] = b2 * vvv[k] + (1.f - b2) * gg[k] * gg[k];
+            pp[k] -= lr_t * mm[k] / (sqrtf(vvv[k]) + eps);
+            o[k] = f2bf(pp[k]);
+        }
+        reinterpret_cast<float4*>(p)[i] = pv;
+        reinterpret_cast<float4*>(m)[i] = mv;
+        reinterpret_cast<float4*>(v)[i] = vv;
+        reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<ushort4*>(pbf)[i] = ob;
+    }
+    // tail
+    for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float gg = g[i];
+        float mm = b1 * m[i] + (1.f - b1) * gg;
+        float vv = b2 * v[i] + (1.f - b2) * gg * gg;
+        float pp = p[i] - lr_t * mm / (sqrtf(vv) + eps);
+        m[i] = mm; v[i] = vv; p[i] = pp; g[i] = 0.f; pbf[i] = f2bf(pp);
+    }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf(x[i]);
+}
+
+void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
+                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream) {
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(1), 0, s, as_ptr<int>(step), as_ptr<float>(lr_t), lr, b1, b2);
+    if (n <= 0) return;
+    int64_t blocks = ((n >> 2) + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, as_ptr<float>(p), as_ptr<float>(g),
+                       as_ptr<float>(m), as_ptr<float>(v), as_ptr<bf16_t>(pbf), as_ptr<const float>(lr_t), n, b1, b2,
+                       eps);
+    SERANN_CHECK(hipGetLastError());
+}
+
+void launch_f32_to_bf16(uint64_t x, uint64_t y, int64_t n, uint64_t stream) {
+    if (n <= 0) return;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                       as_ptr<const float>(x), as_ptr<bf16_t>(y), n);
+    SERANN_CHECK(hipGetLastError());
+}

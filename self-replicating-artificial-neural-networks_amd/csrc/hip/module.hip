@@ -1,0 +1,37 @@
+// pybind11 bindings of the SeRANN-AMD HIP kernels.  Pointers and streams are passed as integers
+// (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream) so that the module has no libtorch
+// ABI dependency; it shares torch's HIP runtime (libamdhip64.so.7 is already loaded by torch).
+#include <pybind11/pybind11.h>
+#include "common.h"
+#include "serann_hip.h"
+
+namespace py = pybind11;
+
+static py::dict desc_sizes() {
+    py::dict d;
+    d["GemmDesc"] = sizeof(GemmDesc);
+    d["ActBwdDesc"] = sizeof(ActBwdDesc);
+    d["BnDesc"] = sizeof(BnDesc);
+    d["PoolDesc"] = sizeof(PoolDesc);
+    d["CopyDesc"] = sizeof(CopyDesc);
+    d["LossDesc"] = sizeof(LossDesc);
+    return d;
+}
+
+PYBIND11_MODULE(serann_hip, m) {
+    m.doc() = "SeRANN-AMD HIP/CDNA4 kernels (gfx950)";
+    m.def("desc_sizes", &desc_sizes);
+    m.def("grouped_gemm", &launch_grouped_gemm, py::arg("mode"), py::arg("descs"), py::arg("tiles"),
+          py::arg("ntiles"), py::arg("stream"));
+    m.def("adam", &launch_adam);
+    m.def("f32_to_bf16", &launch_f32_to_bf16);
+    m.def("gather_batch", &launch_gather_batch);
+    m.def("counter_add", &launch_counter_add);
+    m.def("act_bwd", &launch_act_bwd);
+    m.def("bn", &launch_bn);
+    m.def("pool", &launch_pool);
+    m.def("copy2d", &launch_copy2d);
+    m.def("loss", &launch_loss);
+    m.def("popstats", &launch_popstats);
+    m.def("memset32", &launch_memset32);
+}

@@ -1,0 +1,54 @@
+// Host-side launcher declarations for the SeRANN-AMD HIP kernels (gfx950).
+// All pointers/streams cross the Python boundary as uint64 integers (pybind11 module.hip).
+#pragma once
+#include <stdint.h>
+
+// ---- descriptor layouts (all fields int64 so Python can build them as int64 arrays) ----------
+// Grouped implicit-GEMM convolution problem (see gemm.hip for the per-mode meaning of a/b/out).
+struct GemmDesc {
+    int64_t a, b, out, bias, aux;     // aux: DGRAD/FWD accumulate source (unused = 0)
+    int64_t H, W, C, OH, OW, F, KH, KW, SH, SW;
+    int64_t M, N, K;
+    int64_t act, flags;
+};
+enum GemmFlags : int64_t {
+    GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
+    GF_VEC_B = 2,         // B operand chunks are contiguous 8-element vectors
+    GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
+    GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
+};
+enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+void launch_grouped_gemm(int mode, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+
+// ---- optimizer --------------------------------------------------------------------------------
+void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
+                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream);
+void launch_f32_to_bf16(uint64_t x, uint64_t y, int64_t n, uint64_t stream);
+
+// ---- auxiliary grouped kernels (aux.hip) ------------------------------------------------------
+void launch_gather_batch(uint64_t x_all, uint64_t g_all, uint64_t y_all, uint64_t perm, uint64_t counter,
+                         int64_t base, int64_t B, int64_t n_perm, int64_t x_cols, int64_t g_cols,
+                         uint64_t x_out, uint64_t g_out, uint64_t y_out, uint64_t stream);
+void launch_counter_add(uint64_t counter, int64_t value, uint64_t stream);
+void launch_act_bwd(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_bn(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_pool(int backward, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid);
+void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
+void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
+
+// ---- auxiliary descriptors (int64 fields) ----------------------------------------------------
+struct ActBwdDesc { int64_t dy, y, dz, dbias, M, N, act, flags; };          // flags: 1 = write dz
+struct BnDesc {
+    int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
+    int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx
+    double eps, momentum;
+};
+struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
+struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
+struct LossDesc {
+    int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;
+    double lb;
+};

@@ -1,0 +1,1079 @@
+"""HIP grouped population engine (MI355X / gfx950).
+
+A shard of P heterogeneous organisms is compiled into a *plan*: per dependency level, one grouped
+launch per op kind covering every organism (grouped implicit-GEMM for Dense/Conv2D/Conv1D/heads,
+fused BatchNormalizationF16, MaxPool, concat copies), one fused heads-loss launch, the mirrored
+backward levels, and one fused Keras-Adam launch over a flat fp32 parameter arena.  Architectures
+are fixed for a whole generation, so the training step is captured once into a HIP graph and
+replayed for every one of the ~380 steps (no host work inside the training loop).
+
+Memory (288 GB HBM per MI355X): bf16 activations and activation-gradients for every node at the
+training batch (aliased for reshapes), fp32 master weights + Adam moments + gradients in one arena,
+bf16 compute copy refreshed by the Adam kernel, device-resident datasets (bf16).
+
+Weights use the output-major layout ``Wm[F][KH][KW][C]`` (the forward GEMM's B operand is then
+k-contiguous); the two heads of an organism are stored adjacently as one ``[NC+L][D]`` matrix so
+they run as a single GEMM with an fp32 output.
+
+Rare ops reachable only by mutation (unary/binary minus, BatchNormalization on a non-last axis)
+run through a torch fallback inside the same plan (still graph-captured).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..genome.ir import Node, OrganismIR
+from ..models.organism import glorot_limit, init_params
+from ..ops import hip_ops as H
+from .base import FitResult, PopulationEngine, TrainConfig, epoch_permutation
+
+ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp32
+
+
+def _al(n: int) -> int:
+    return (int(n) + ALIGN - 1) // ALIGN * ALIGN
+
+
+class Arena:
+    """Bump allocator over one device tensor."""
+
+    def __init__(self, dtype, device):
+        self.dtype, self.device = dtype, device
+        self.size = 0
+        self.t: Optional[torch.Tensor] = None
+
+    def alloc(self, n: int) -> int:
+        off = self.size
+        self.size += _al(max(1, n))
+        return off
+
+    def materialize(self, zero=True):
+        self.t = (torch.zeros if zero else torch.empty)(max(self.size, ALIGN), dtype=self.dtype, device=self.device)
+        return self.t
+
+    def view(self, off: int, n: int) -> torch.Tensor:
+        return self.t.narrow(0, off, n)
+
+    def ptr(self, off: int) -> int:
+        return self.t.data_ptr() + off * self.t.element_size()
+
+
+_DEVICE_DATA: Dict[Tuple[int, str], dict] = {}
+
+
+def device_data(data, device) -> dict:
+    """Upload the (shared) training/test arrays once per process, as bf16 / int32."""
+    key = (id(data), str(device))
+    d = _DEVICE_DATA.get(key)
+    if d is None:
+        def bf(a):
+            return torch.as_tensor(np.ascontiguousarray(a.reshape(len(a), -1)), dtype=torch.float32).to(
+                device).to(torch.bfloat16).contiguous()
+
+        d = {
+            "train_x": bf(data.train_x), "train_g": bf(data.train_g),
+            "train_y": torch.as_tensor(data.train_labels.astype(np.int32), device=device),
+            "test_x": bf(data.test_x), "test_g": bf(data.test_g),
+            "test_y": torch.as_tensor(data.test_labels.astype(np.int32), device=device),
+        }
+        _DEVICE_DATA[key] = d
+    return d
+
+
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class OrgLayout:
+    """Per-organism parameter / buffer layout (offsets into the arenas)."""
+    ir: OrganismIR
+    w: Dict[int, int] = field(default_factory=dict)       # gemm node -> Wm offset (param arena)
+    b: Dict[int, int] = field(default_factory=dict)       # gemm node -> bias offset
+    gamma: Dict[int, int] = field(default_factory=dict)
+    beta: Dict[int, int] = field(default_factory=dict)
+    mm: Dict[int, int] = field(default_factory=dict)      # moving stats (stat arena)
+    mv: Dict[int, int] = field(default_factory=dict)
+    head: int = -1                                         # fused head pseudo-node id
+
+
+@dataclass
+class Launch:
+    kind: str
+    arg: int
+    descs: Optional[torch.Tensor]
+    tiles: Optional[torch.Tensor]
+    n: int
+    fn: object = None
+
+
+class Plan:
+    """A compiled list of launches for one (mode, batch) configuration."""
+
+    def __init__(self):
+        self.launches: List[Launch] = []
+        self.keep: List[torch.Tensor] = []
+
+    def run(self):
+        L = H.lib()
+        s = H.stream_handle()
+        for la in self.launches:
+            k = la.kind
+            if k == "gemm":
+                L.grouped_gemm(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "act_bwd":
+                L.act_bwd(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "bn":
+                L.bn(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "pool":
+                L.pool(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "copy":
+                L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "fn":
+                la.fn()
+            else:
+                raise ValueError(k)
+
+
+class HipPopulationEngine(PopulationEngine):
+    def __init__(self, irs: Sequence[OrganismIR], seeds: Sequence[int], device="cuda", cfg: Optional[TrainConfig] = None,
+                 params: Optional[List[Dict[int, Dict[str, np.ndarray]]]] = None):
+        self.lib = H.lib(required=True)
+        H.check_layouts()
+        self.device = torch.device(device)
+        self.cfg = cfg or TrainConfig()
+        self.irs = list(irs)
+        self.num_organisms = len(self.irs)
+        self.lb = [float(ir.loss_balance) for ir in self.irs]
+        self._build_param_layout()
+        self._init_params(seeds, params)
+        self.plans: Dict[tuple, Plan] = {}
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.timings: Dict[str, float] = {}
+
+    # ---------------------------------------------------------------------------------------------
+    # parameters
+    # ---------------------------------------------------------------------------------------------
+    def _build_param_layout(self):
+        dev = self.device
+        self.parena = Arena(torch.float32, dev)
+        self.sarena = Arena(torch.float32, dev)     # BN moving statistics
+        self.layouts: List[OrgLayout] = []
+        for ir in self.irs:
+            lay = OrgLayout(ir)
+            for n in ir.nodes:
+                if n.op == "gemm" and n.attrs["kind"] not in ("head_cls", "head_rep"):
+                    a = n.attrs
+                    lay.w[n.id] = self.parena.alloc(a["f"] * a["kh"] * a["kw"] * a["cin"])
+                    if a["use_bias"]:
+                        lay.b[n.id] = self.parena.alloc(a["f"])
+                elif n.op == "bn":
+                    c = n.attrs["channels"]
+                    if n.attrs["scale"]:
+                        lay.gamma[n.id] = self.parena.alloc(c)
+                    if n.attrs["center"]:
+                        lay.beta[n.id] = self.parena.alloc(c)
+                    lay.mm[n.id] = self.sarena.alloc(c)
+                    lay.mv[n.id] = self.sarena.alloc(c)
+            # fused heads: [NC + L][D] contiguous, bias [NC + L]
+            D, NC, L = ir.head_features, ir.num_classes, ir.genotype_size
+            lay.head = ir.cls_head
+            lay.w[ir.cls_head] = self.parena.alloc((NC + L) * D)
+            lay.b[ir.cls_head] = self.parena.alloc(NC + L)
+            self.layouts.append(lay)
+        self.p = self.parena.materialize()
+        self.g = torch.zeros_like(self.p)
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p)
+        self.pbf = torch.zeros(self.p.numel(), dtype=torch.bfloat16, device=dev)
+        self.stats = self.sarena.materialize()
+        self.step_i = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr_t = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    def _init_params(self, seeds, params):
+        """Keras defaults: glorot-uniform kernels, zero bias, gamma 1, beta 0, moving var 1.
+        With ``params`` (numpy, Keras layout) the exact values are loaded (parity tests)."""
+        P = self.p
+        with torch.no_grad():
+            for i, lay in enumerate(self.layouts):
+                ir = lay.ir
+                gen = torch.Generator(device=self.device)
+                gen.manual_seed(int(seeds[i]) if seeds is not None else i)
+                src = params[i] if params is not None else None
+                for n in ir.nodes:
+                    if n.op == "gemm":
+                        a = n.attrs
+                        if a["kind"] == "head_rep":
+                            continue
+                        if a["kind"] == "head_cls":
+                            D, NC, L = ir.head_features, ir.num_classes, ir.genotype_size
+                            rep = ir.node(ir.rep_head)
+                            blocks = []
+                            for hn in (n, rep):
+                                ha = hn.attrs
+                                if src is not None:
+                                    k = torch.as_tensor(src[hn.id]["kernel"], device=self.device)   # (1,1,D,f)
+                                    blocks.append(k.reshape(D, ha["f"]).t())
+                                else:
+                                    lim = glorot_limit(hn)
+                                    blocks.append((torch.rand(ha["f"], D, generator=gen, device=self.device) * 2 - 1) * lim)
+                            w = torch.cat(blocks, 0)
+                            P.narrow(0, lay.w[n.id], (NC + L) * D).copy_(w.reshape(-1))
+                            P.narrow(0, lay.b[n.id], NC + L).zero_()
+                            continue
+                        cnt = a["f"] * a["kh"] * a["kw"] * a["cin"]
+                        if src is not None:
+                            k = torch.as_tensor(src[n.id]["kernel"], device=self.device)   # (kh,kw,c,f)
+                            w = k.permute(3, 0, 1, 2).reshape(-1)
+                        else:
+                            w = (torch.rand(cnt, generator=gen, device=self.device) * 2 - 1) * glorot_limit(n)
+                        P.narrow(0, lay.w[n.id], cnt).copy_(w)
+                        if n.id in lay.b:
+                            P.narrow(0, lay.b[n.id], a["f"]).zero_()
+                    elif n.op == "bn":
+                        c = n.attrs["channels"]
+                        if n.id in lay.gamma:
+                            P.narrow(0, lay.gamma[n.id], c).fill_(1.0)
+                        if n.id in lay.beta:
+                            P.narrow(0, lay.beta[n.id], c).zero_()
+                        self.stats.narrow(0, lay.mm[n.id], c).zero_()
+                        self.stats.narrow(0, lay.mv[n.id], c).fill_(1.0)
+            self.pbf.copy_(P.to(torch.bfloat16))
+
+    def export_params(self, i: int) -> Dict[int, Dict[str, np.ndarray]]:
+        """Organism ``i`` parameters in Keras layout (for parity tests / checkpoints)."""
+        lay = self.layouts[i]
+        ir = lay.ir
+        out: Dict[int, Dict[str, np.ndarray]] = {}
+        P, S = self.p.detach().cpu(), self.stats.detach().cpu()
+        for n in ir.nodes:
+            a = n.attrs
+            if n.op == "gemm":
+                if a["kind"] in ("head_cls", "head_rep"):
+                    D, NC, L = ir.head_features, ir.num_classes, ir.genotype_size
+                    w = P.narrow(0, lay.w[ir.cls_head], (NC + L) * D).reshape(NC + L, D)
+                    b = P.narrow(0, lay.b[ir.cls_head], NC + L)
+                    sl = slice(0, NC) if a["kind"] == "head_cls" else slice(NC, NC + L)
+                    out[n.id] = {"kernel": w[sl].t().reshape(1, 1, D, -1).numpy().copy(), "bias": b[sl].numpy().copy()}
+                    continue
+                cnt = a["f"] * a["kh"] * a["kw"] * a["cin"]
+                w = P.narrow(0, lay.w[n.id], cnt).reshape(a["f"], a["kh"], a["kw"], a["cin"]).permute(1, 2, 3, 0)
+                d = {"kernel": w.numpy().copy()}
+                if n.id in lay.b:
+                    d["bias"] = P.narrow(0, lay.b[n.id], a["f"]).numpy().copy()
+                out[n.id] = d
+            elif n.op == "bn":
+                c = a["channels"]
+                d = {"moving_mean": S.narrow(0, lay.mm[n.id], c).numpy().copy(),
+                     "moving_variance": S.narrow(0, lay.mv[n.id], c).numpy().copy()}
+                if n.id in lay.gamma:
+                    d["gamma"] = P.narrow(0, lay.gamma[n.id], c).numpy().copy()
+                if n.id in lay.beta:
+                    d["beta"] = P.narrow(0, lay.beta[n.id], c).numpy().copy()
+                out[n.id] = d
+        return out
+
+    # ---------------------------------------------------------------------------------------------
+    # activation buffers
+    # ---------------------------------------------------------------------------------------------
+    def _alloc_buffers(self, B: int, with_grads: bool):
+        """Activation (and gradient) buffers for batch B; aliases for reshapes."""
+        dev = self.device
+        act = Arena(torch.bfloat16, dev)
+        grad = Arena(torch.bfloat16, dev)
+        f32 = Arena(torch.float32, dev)
+        u8 = Arena(torch.uint8, dev)
+        bufs = []
+        for lay in self.layouts:
+            ir = lay.ir
+            bmap = {}
+            owner = {}
+            for n in ir.nodes:
+                size = B * math.prod(n.shape)
+                if n.op == "input":
+                    owner[n.id] = n.id
+                    continue
+                if n.op == "reshape":
+                    owner[n.id] = owner[n.inputs[0]]
+                    bmap[n.id] = bmap.get(n.inputs[0])
+                    continue
+                if n.op == "gemm" and n.attrs["kind"] == "head_rep":
+                    continue
+                owner[n.id] = n.id
+                if n.op == "gemm" and n.attrs["kind"] == "head_cls":
+                    NC, L = ir.num_classes, ir.genotype_size
+                    bmap[n.id] = ("f32", f32.alloc(B * (NC + L)))
+                    continue
+                bmap[n.id] = ("act", act.alloc(size))
+            rec = {"owner": owner, "act": bmap, "grad": {}, "idx": {}, "bn": {}}
+            for n in ir.nodes:
+                if n.op == "pool":
+                    rec["idx"][n.id] = u8.alloc(B * math.prod(n.shape))
+                if n.op == "bn":
+                    c = n.attrs["channels"]
+                    rec["bn"][n.id] = {"mean": f32.alloc(c), "invstd": f32.alloc(c), "ws": None, "wsb": None}
+            if with_grads:
+                req = self._requires_grad(ir)
+                for n in ir.nodes:
+                    if n.op in ("input", "reshape") or (n.op == "gemm" and n.attrs["kind"] == "head_rep"):
+                        continue
+                    if n.op == "gemm" and n.attrs["kind"] == "head_cls":
+                        NC, L = ir.num_classes, ir.genotype_size
+                        rec["grad"][n.id] = grad.alloc(B * (NC + L))
+                    elif req[n.id]:
+                        rec["grad"][n.id] = grad.alloc(B * math.prod(n.shape))
+                rec["req"] = req
+            bufs.append(rec)
+        # BN workspaces contiguous so one memset zeroes them all
+        ws = Arena(torch.float32, dev)
+        for lay, rec in zip(self.layouts, bufs):
+            for nid, d in rec["bn"].items():
+                c = lay.ir.node(nid).attrs["channels"]
+                d["ws"] = ws.alloc(2 * c)
+                d["wsb"] = ws.alloc(2 * c)
+        act.materialize(zero=True)
+        grad.materialize(zero=True)
+        f32.materialize(zero=True)
+        u8.materialize(zero=True)
+        ws.materialize(zero=True)
+        return {"act": act, "grad": grad, "f32": f32, "u8": u8, "ws": ws, "orgs": bufs, "B": B}
+
+    @staticmethod
+    def _requires_grad(ir: OrganismIR) -> Dict[int, bool]:
+        req = {}
+        for n in ir.nodes:
+            if n.op == "input":
+                req[n.id] = False
+            elif n.op == "reshape":
+                req[n.id] = req[n.inputs[0]]
+            else:
+                has_params = n.op == "gemm" or (n.op == "bn" and (n.attrs["scale"] or n.attrs["center"]))
+                req[n.id] = has_params or any(req[i] for i in n.inputs)
+        return req
+
+    # ---------------------------------------------------------------------------------------------
+    # plan compilation
+    # ---------------------------------------------------------------------------------------------
+    def _act_ptr(self, mem, org: int, nid: int, inputs: dict) -> int:
+        rec = mem["orgs"][org]
+        ir = self.layouts[org].ir
+        own = rec["owner"][nid]
+        node = ir.node(own)
+        if node.op == "input":
+            return inputs[org][node.attrs["name"]]
+        kind, off = rec["act"][own]
+        return mem["act"].ptr(off) if kind == "act" else mem["f32"].ptr(off)
+
+    def _grad_ptr(self, mem, org: int, nid: int) -> int:
+        rec = mem["orgs"][org]
+        own = rec["owner"][nid]
+        off = rec["grad"].get(own)
+        return None if off is None else mem["grad"].ptr(off)
+
+    def _build_plan(self, mode: str, B: int, mem, inputs: List[dict], label_ptr: int = 0, target_ptrs=None,
+                    metrics: Optional[torch.Tensor] = None) -> Plan:
+        """mode in {'train', 'infer'}; inputs[org] = {'X': ptr, 'g': ptr} bf16 device pointers."""
+        train = mode == "train"
+        plan = Plan()
+        P = self.num_organisms
+        depth_of = []
+        maxd = 0
+        for lay in self.layouts:
+            dd = {}
+            for n in lay.ir.nodes:
+                dd[n.id] = 0 if n.op == "input" else 1 + max(dd[i] for i in n.inputs)
+            depth_of.append(dd)
+            maxd = max(maxd, max(dd.values()))
+
+        def T(arr, dtype=None):
+            t = torch.as_tensor(arr, device=self.device) if dtype is None else torch.as_tensor(arr, dtype=dtype,
+                                                                                               device=self.device)
+            plan.keep.append(t)
+            return t
+
+        def desc_tensor(rows, dtype):
+            a = np.zeros(len(rows), dtype=dtype)
+            for i, r in enumerate(rows):
+                for k, v in r.items():
+                    a[i][k] = v
+            return T(np.frombuffer(a.tobytes(), dtype=np.uint8).copy())
+
+        def add_gemm(mode_, rows, dims):
+            if not rows:
+                return
+            tiles = H.gemm_tiles(dims, mode_)
+            if len(tiles) == 0:
+                return
+            plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
+
+        def add_chunked(kind, arg, rows, dtype, counts, chunk):
+            if not rows:
+                return
+            tiles = H.chunk_tiles(counts, chunk)
+            if len(tiles) == 0:
+                return
+            plan.launches.append(Launch(kind, arg, desc_tensor(rows, dtype), T(tiles), len(tiles)))
+
+        pa, pbf = self.parena, self.pbf
+
+        def wptr_bf(off):
+            return pbf.data_ptr() + off * 2
+
+        def pptr(off):
+            return self.p.data_ptr() + off * 4
+
+        def gptr(off):
+            return self.g.data_ptr() + off * 4
+
+        def sptr(off):
+            return self.stats.data_ptr() + off * 4
+
+        f32a = mem["f32"]
+
+        # ---- forward ---------------------------------------------------------------------------
+        for d in range(1, maxd + 1):
+            g_rows, g_dims = [], []
+            p_rows, p_cnt = [], []
+            bn_rows, bn_cnt = [], []
+            c_rows, c_cnt = [], []
+            fallbacks = []
+            for o, lay in enumerate(self.layouts):
+                ir = lay.ir
+                rec = mem["orgs"][o]
+                for n in ir.nodes:
+                    if depth_of[o][n.id] != d or n.op in ("input", "reshape"):
+                        continue
+                    a = n.attrs
+                    if n.op == "gemm":
+                        if a["kind"] == "head_rep":
+                            continue
+                        xin = self._act_ptr(mem, o, n.inputs[0], inputs)
+                        out = self._act_ptr(mem, o, n.id, inputs)
+                        if a["kind"] == "head_cls":
+                            NC, L, D = ir.num_classes, ir.genotype_size, ir.head_features
+                            F, C, flags, act = NC + L, D, H.GF_OUT_F32, 0
+                            Hh = Ww = OH = OW = 1
+                            KH = KW = SH = SW = 1
+                        else:
+                            F, C = a["f"], a["cin"]
+                            Hh, Ww, OH, OW = a["h"], a["w"], a["oh"], a["ow"]
+                            KH, KW, SH, SW = a["kh"], a["kw"], a["sh"], a["sw"]
+                            flags, act = 0, H.ACT_CODES[a["act"]]
+                        K = KH * KW * C
+                        M = B * OH * OW
+                        if C % 8 == 0:
+                            flags |= H.GF_VEC_A
+                        if K % 8 == 0:
+                            flags |= H.GF_VEC_B
+                        bias = pptr(lay.b[n.id]) if n.id in lay.b else 0
+                        g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
+                                           OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
+                                           flags=flags))
+                        g_dims.append((M, F, K))
+                    elif n.op == "pool":
+                        p_rows.append(dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
+                                           y=self._act_ptr(mem, o, n.id, inputs),
+                                           idx=mem["u8"].ptr(rec["idx"][n.id]), B=B, H=a["h"], W=a["w"], C=a["c"],
+                                           OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"]))
+                        p_cnt.append(B * math.prod(n.shape))
+                    elif n.op == "bn" and a["last"]:
+                        bd = rec["bn"][n.id]
+                        c = a["channels"]
+                        flags = (1 if n.id in lay.gamma else 0) | (2 if n.id in lay.beta else 0)
+                        bn_rows.append(dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
+                                            y=self._act_ptr(mem, o, n.id, inputs),
+                                            gamma=pptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                            beta=pptr(lay.beta[n.id]) if n.id in lay.beta else 0,
+                                            mm=sptr(lay.mm[n.id]), mv=sptr(lay.mv[n.id]),
+                                            mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
+                                            ws=mem["ws"].ptr(bd["ws"]), R=B * math.prod(n.shape) // c, C=c,
+                                            flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
+                        bn_cnt.append(B * math.prod(n.shape) // c)
+                    elif n.op == "concat":
+                        ax = a["axis"]
+                        outer = B * math.prod(n.shape[:ax - 1])
+                        out_inner = math.prod(n.shape[ax - 1:])
+                        col = 0
+                        for i in n.inputs:
+                            sh = ir.node(i).shape
+                            inner = math.prod(sh[ax - 1:])
+                            c_rows.append(dict(src=self._act_ptr(mem, o, i, inputs),
+                                               dst=self._act_ptr(mem, o, n.id, inputs) + col * 2,
+                                               rows=outer, cols=inner, src_stride=inner, dst_stride=out_inner))
+                            c_cnt.append(outer * inner)
+                            col += inner
+                    else:
+                        fallbacks.append((o, n))
+            add_gemm(H.MODE_FWD, g_rows, g_dims)
+            add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
+            if bn_rows:
+                if train:
+                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
+                    add_chunked("bn", 1, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
+                    add_chunked("bn", 2, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
+                else:
+                    add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
+            add_chunked("copy", 0, c_rows, H.COPY_DTYPE, c_cnt, H.COPY_ELEMS)
+            for o, n in fallbacks:
+                plan.launches.append(Launch("fn", 0, None, None, 0, self._fallback_fwd(mem, o, n, inputs, B, train)))
+
+        # ---- loss ------------------------------------------------------------------------------
+        if metrics is not None:
+            rows = []
+            for o, lay in enumerate(self.layouts):
+                ir = lay.ir
+                rec = mem["orgs"][o]
+                NC, L = ir.num_classes, ir.genotype_size
+                rows.append(dict(logits=self._act_ptr(mem, o, ir.cls_head, inputs),
+                                 dlogits=mem["grad"].ptr(rec["grad"][ir.cls_head]) if train else 0,
+                                 labels=label_ptr, target=target_ptrs[o], metrics=metrics.data_ptr() + 16 * o,
+                                 NC=NC, L=L, B=B, lb=self.lb[o]))
+            plan.loss = (desc_tensor(rows, H.LOSS_DTYPE), P, B)
+        else:
+            plan.loss = None
+
+        plan.fwd_count = len(plan.launches)
+        if not train:
+            return plan
+
+        # ---- backward --------------------------------------------------------------------------
+        # Gradient buffers are written by several op kinds; the first writer of a buffer (in
+        # execution order) overwrites it and later writers accumulate.  Two writers of one buffer
+        # never share a launch.
+        written = [set() for _ in range(P)]
+
+        def target(o, nid):
+            rec = mem["orgs"][o]
+            own = rec["owner"][nid]
+            if not rec["req"].get(own, False):
+                return None
+            return own
+
+        STAGES = ("dgrad", "pool", "bn", "copy")
+        for d in range(maxd, 0, -1):
+            ab_rows, ab_cnt = [], []
+            wg_rows, wg_dims = [], []
+            bn_red, bn_red_cnt = [], []
+            tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
+            fb = []
+            for o, lay in enumerate(self.layouts):
+                ir = lay.ir
+                rec = mem["orgs"][o]
+                for n in ir.nodes:
+                    if depth_of[o][n.id] != d or n.op in ("input", "reshape"):
+                        continue
+                    if n.op == "gemm" and n.attrs["kind"] == "head_rep":
+                        continue
+                    a = n.attrs
+                    if not rec["req"].get(n.id, False):
+                        continue
+                    if n.op == "gemm":
+                        head = a["kind"] == "head_cls"
+                        dz = mem["grad"].ptr(rec["grad"][n.id])
+                        yv = self._act_ptr(mem, o, n.id, inputs)
+                        if head:
+                            NC, L, D = ir.num_classes, ir.genotype_size, ir.head_features
+                            F, C, act = NC + L, D, 0
+                            Hh = Ww = OH = OW = 1
+                            KH = KW = SH = SW = 1
+                        else:
+                            F, C = a["f"], a["cin"]
+                            Hh, Ww, OH, OW = a["h"], a["w"], a["oh"], a["ow"]
+                            KH, KW, SH, SW = a["kh"], a["kw"], a["sh"], a["sw"]
+                            act = H.ACT_CODES[a["act"]]
+                        M = B * OH * OW
+                        K = KH * KW * C
+                        dbias = gptr(lay.b[n.id]) if n.id in lay.b else 0
+                        if act != 0 or dbias:
+                            ab_rows.append(dict(dy=dz, y=yv, dz=dz, dbias=dbias, M=M, N=F, act=act,
+                                                flags=1 if act != 0 else 0))
+                            ab_cnt.append(M)
+                        xin = self._act_ptr(mem, o, n.inputs[0], inputs)
+                        vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
+                        wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
+                                            KH=KH, KW=KW, SH=SH, SW=SW, M=F, N=K, K=M, flags=vec))
+                        wg_dims.append((F, K, M))
+                        own = target(o, n.inputs[0])
+                        if own is not None:
+                            Mi = B * Hh * Ww
+                            base = dict(a=dz, b=wptr_bf(lay.w[n.id]), out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
+                                        W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,
+                                        K=KH * KW * F)
+                            tasks["dgrad"].append((o, own, lambda acc, r=base, v=vec: dict(r, flags=v | (H.GF_ACCUM if acc else 0)),
+                                                   (Mi, C, KH * KW * F)))
+                    elif n.op == "pool":
+                        own = target(o, n.inputs[0])
+                        if own is not None:
+                            base = dict(idx=mem["u8"].ptr(rec["idx"][n.id]), dy=mem["grad"].ptr(rec["grad"][n.id]),
+                                        dx=mem["grad"].ptr(rec["grad"][own]), B=B, H=a["h"], W=a["w"], C=a["c"],
+                                        OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"])
+                            tasks["pool"].append((o, own, lambda acc, r=base: dict(r, flags=1 if acc else 0),
+                                                  B * a["h"] * a["w"] * a["c"]))
+                    elif n.op == "bn" and a["last"]:
+                        bd = rec["bn"][n.id]
+                        c = a["channels"]
+                        R = B * math.prod(n.shape) // c
+                        own = target(o, n.inputs[0])
+                        pflags = (1 if n.id in lay.gamma else 0) | (2 if n.id in lay.beta else 0)
+                        base = dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
+                                    dy=mem["grad"].ptr(rec["grad"][n.id]),
+                                    dx=mem["grad"].ptr(rec["grad"][own]) if own is not None else 0,
+                                    gamma=pptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                    mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
+                                    ws=mem["ws"].ptr(bd["wsb"]),
+                                    dgamma=gptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                    dbeta=gptr(lay.beta[n.id]) if n.id in lay.beta else 0,
+                                    R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
+                        bn_red.append(dict(base, flags=pflags))
+                        bn_red_cnt.append(R)
+                        if own is None:
+                            tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8), R))
+                        else:
+                            tasks["bn"].append((o, own, lambda acc, r=base, f=pflags: dict(r, flags=f | (4 if acc else 0)), R))
+                    elif n.op == "concat":
+                        ax = a["axis"]
+                        outer = B * math.prod(n.shape[:ax - 1])
+                        out_inner = math.prod(n.shape[ax - 1:])
+                        col = 0
+                        dyp = mem["grad"].ptr(rec["grad"][n.id])
+                        for i in n.inputs:
+                            inner = math.prod(ir.node(i).shape[ax - 1:])
+                            own = target(o, i)
+                            if own is not None:
+                                base = dict(src=dyp + col * 2, dst=mem["grad"].ptr(rec["grad"][own]), rows=outer,
+                                            cols=inner, src_stride=out_inner, dst_stride=inner)
+                                tasks["copy"].append((o, own, lambda acc, r=base: dict(r, flags=1 if acc else 0),
+                                                      outer * inner))
+                            col += inner
+                    else:
+                        fb.append((o, n))
+            add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, H.ACT_ROWS)
+            add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
+            if bn_red:
+                add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, H.BN_ROWS)
+            for stage in STAGES:
+                batches = [[]]
+                used = [set()]
+                for o, own, make, cnt in tasks[stage]:
+                    key = (o, own) if own is not None else None
+                    if key is not None and key in used[-1]:
+                        batches.append([])
+                        used.append(set())
+                    acc = own is not None and own in written[o]
+                    batches[-1].append((make(acc), cnt))
+                    if key is not None:
+                        used[-1].add(key)
+                        written[o].add(own)
+                for b in batches:
+                    if not b:
+                        continue
+                    rows = [r for r, _ in b]
+                    cnts = [c for _, c in b]
+                    if stage == "dgrad":
+                        add_gemm(H.MODE_DGRAD, rows, cnts)
+                    elif stage == "pool":
+                        add_chunked("pool", 1, rows, H.POOL_DTYPE, cnts, H.POOL_ELEMS)
+                    elif stage == "bn":
+                        add_chunked("bn", 5, rows, H.BN_DTYPE, cnts, H.BN_ROWS)
+                    else:
+                        add_chunked("copy", 0, rows, H.COPY_DTYPE, cnts, H.COPY_ELEMS)
+            for o, n in fb:
+                plan.launches.append(Launch("fn", 0, None, None, 0,
+                                            self._fallback_bwd(mem, o, n, inputs, B, target, written)))
+        return plan
+
+    # ---------------------------------------------------------------------------------------------
+    # torch fallback for rare ops (neg / sub / BN on a non-last axis)
+    # ---------------------------------------------------------------------------------------------
+    def _view(self, mem, o, nid, inputs, B, grad=False):
+        ir = self.layouts[o].ir
+        n = ir.node(nid)
+        numel = B * math.prod(n.shape)
+        if grad:
+            p = self._grad_ptr(mem, o, nid)
+            arena, base = mem["grad"], mem["grad"].t
+        else:
+            p = self._act_ptr(mem, o, nid, inputs)
+            arena, base = mem["act"], mem["act"].t
+        off = (p - base.data_ptr()) // 2
+        if 0 <= off < base.numel():
+            return base.narrow(0, off, numel).view((B,) + n.shape)
+        # raw input buffers live outside the arena
+        t = self._input_tensors[p]
+        return t.reshape(-1).narrow(0, 0, numel).view((B,) + n.shape)
+
+    def _fallback_compute(self, o, n, xs, training):
+        a = n.attrs
+        lay = self.layouts[o]
+        if n.op == "neg":
+            return -xs[0]
+        if n.op == "sub":
+            m = a["mode"]
+            return xs[0] - xs[1] if m == "tt" else (xs[0] - a["c"] if m == "tc" else a["c"] - xs[0])
+        if n.op == "bn":
+            ax = a["axis"]
+            x = xs[0]
+            red = [i for i in range(x.dim()) if i != ax]
+            shp = [1] * x.dim()
+            shp[ax] = a["channels"]
+            c = a["channels"]
+            gamma = self.p.narrow(0, lay.gamma[n.id], c) if n.id in lay.gamma else None
+            beta = self.p.narrow(0, lay.beta[n.id], c) if n.id in lay.beta else None
+            mm = self.stats.narrow(0, lay.mm[n.id], c)
+            mv = self.stats.narrow(0, lay.mv[n.id], c)
+            if training:
+                mean = x.mean(red)
+                var = x.var(red, unbiased=False)
+                y = (x - mean.view(shp)) / torch.sqrt(var.view(shp) + a["epsilon"])
+            else:
+                y = (x - mm.view(shp)) / torch.sqrt(mv.view(shp) + a["epsilon"])
+            if gamma is not None:
+                y = y * gamma.view(shp)
+            if beta is not None:
+                y = y + beta.view(shp)
+            return y, (mean, var) if training else None
+        raise ValueError(n.op)
+
+    def _fallback_fwd(self, mem, o, n, inputs, B, train):
+        def fn():
+            xs = [self._view(mem, o, i, inputs, B).float() for i in n.inputs]
+            out = self._fallback_compute(o, n, xs, train)
+            if n.op == "bn":
+                y, st = out
+                if train and st is not None:
+                    a = n.attrs
+                    lay = self.layouts[o]
+                    c = a["channels"]
+                    mean, var = st
+                    nsamp = float(B * math.prod(n.shape) // c)
+                    mom = a["momentum"]
+                    mm = self.stats.narrow(0, lay.mm[n.id], c)
+                    mv = self.stats.narrow(0, lay.mv[n.id], c)
+                    mm.mul_(mom).add_(mean * (1 - mom))
+                    mv.mul_(mom).add_(var * (nsamp / (nsamp - (1 + a["epsilon"]))) * (1 - mom))
+                out = y
+            self._view(mem, o, n.id, inputs, B).copy_(out.to(torch.bfloat16))
+        return fn
+
+    def _fallback_bwd(self, mem, o, n, inputs, B, target, written):
+        tgs = []
+        for i in n.inputs:
+            own = target(o, i)
+            tgs.append(None if own is None else (own, own in written[o]))
+            if own is not None:
+                written[o].add(own)
+        lay = self.layouts[o]
+
+        def fn():
+            xs = [self._view(mem, o, i, inputs, B).float().requires_grad_(True) for i in n.inputs]
+            params = []
+            if n.op == "bn":
+                c = n.attrs["channels"]
+                for d in (lay.gamma, lay.beta):
+                    if n.id in d:
+                        params.append(self.p.narrow(0, d[n.id], c).detach().clone().requires_grad_(True))
+            with torch.enable_grad():
+                out = self._fallback_compute_params(o, n, xs, params)
+                dy = self._view(mem, o, n.id, inputs, B, grad=True).float()
+                grads = torch.autograd.grad(out, xs + params, dy, allow_unused=True)
+            for x_i, gi, tg in zip(n.inputs, grads[:len(xs)], tgs):
+                if tg is None or gi is None:
+                    continue
+                own, acc = tg
+                rec = mem["orgs"][o]
+                dst = mem["grad"].t.narrow(0, (mem["grad"].ptr(rec["grad"][own]) - mem["grad"].t.data_ptr()) // 2,
+                                           gi.numel())
+                g = gi.reshape(-1)
+                if g.numel() != dst.numel():
+                    # broadcast-reduced operand
+                    g = gi.sum_to_size(self._view(mem, o, own, inputs, B).shape).reshape(-1)
+                if acc:
+                    dst.copy_((dst.float() + g).to(torch.bfloat16))
+                else:
+                    dst.copy_(g.to(torch.bfloat16))
+            k = len(xs)
+            if n.op == "bn":
+                c = n.attrs["channels"]
+                for d in (lay.gamma, lay.beta):
+                    if n.id in d:
+                        gg = grads[k]
+                        k += 1
+                        if gg is not None:
+                            self.g.narrow(0, d[n.id], c).add_(gg)
+        return fn
+
+    def _fallback_compute_params(self, o, n, xs, params):
+        if n.op != "bn":
+            return self._fallback_compute(o, n, xs, True)
+        a = n.attrs
+        lay = self.layouts[o]
+        x = xs[0]
+        ax = a["axis"]
+        red = [i for i in range(x.dim()) if i != ax]
+        shp = [1] * x.dim()
+        shp[ax] = a["channels"]
+        mean = x.mean(red)
+        var = x.var(red, unbiased=False)
+        y = (x - mean.view(shp)) / torch.sqrt(var.view(shp) + a["epsilon"])
+        k = 0
+        if n.id in lay.gamma:
+            y = y * params[k].view(shp)
+            k += 1
+        if n.id in lay.beta:
+            y = y + params[k].view(shp)
+        return y
+
+    # ---------------------------------------------------------------------------------------------
+    # execution
+    # ---------------------------------------------------------------------------------------------
+    def _run_loss(self, plan: Plan, train: bool, nvalid: int):
+        if plan.loss is None:
+            return
+        descs, P, B = plan.loss
+        self.lib.loss(1 if train else 0, descs.data_ptr(), P, B, H.stream_handle(), nvalid)
+
+    def fit(self, data, cfg: Optional[TrainConfig] = None) -> FitResult:
+        cfg = cfg or self.cfg
+        dev = self.device
+        dd = device_data(data, dev)
+        P = self.num_organisms
+        n = dd["train_x"].shape[0]
+        split = cfg.split(n)
+        steps = cfg.steps_per_epoch(split)
+        B = cfg.batch_size
+        xcols, gcols = dd["train_x"].shape[1], dd["train_g"].shape[1]
+
+        # shared batch buffers
+        xb = torch.zeros(B, xcols, dtype=torch.bfloat16, device=dev)
+        gb = torch.zeros(B, gcols, dtype=torch.bfloat16, device=dev)
+        yb = torch.zeros(B, dtype=torch.int32, device=dev)
+        self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
+        perm_t = torch.zeros(max(split, 1), dtype=torch.int32, device=dev)
+        counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        metrics = torch.zeros(P, 4, dtype=torch.float32, device=dev)
+
+        t_plan = time.perf_counter()
+        mem = self._alloc_buffers(B, with_grads=True)
+        self._train_mem = mem
+        inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(P)]
+        targets = [gb.data_ptr()] * P
+        plan = self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics)
+        L = self.lib
+        ws = mem["ws"].t
+
+        def step():
+            s = H.stream_handle()
+            L.gather_batch(dd["train_x"].data_ptr(), dd["train_g"].data_ptr(), dd["train_y"].data_ptr(),
+                           perm_t.data_ptr(), counter.data_ptr(), 0, B, split, xcols, gcols, xb.data_ptr(),
+                           gb.data_ptr(), yb.data_ptr(), s)
+            L.memset32(ws.data_ptr(), ws.numel(), s)
+            fwd = plan.launches[:plan.fwd_count]
+            bwd = plan.launches[plan.fwd_count:]
+            tmp = Plan()
+            tmp.launches = fwd
+            tmp.run()
+            self._run_loss(plan, True, B)
+            tmp.launches = bwd
+            tmp.run()
+            L.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
+                   self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), cfg.lr, cfg.beta1, cfg.beta2,
+                   cfg.eps, s)
+            L.counter_add(counter.data_ptr(), 1, s)
+
+        use_graph = split % B == 0 and steps == split // B
+        graph = None
+        self.timings["plan_s"] = time.perf_counter() - t_plan
+        self.timings["launches_per_step"] = len(plan.launches) + 5
+
+        t0 = time.perf_counter()
+        train_acc = np.zeros(P)
+        val_acc = np.full(P, np.nan)
+        val_mse = np.full(P, np.nan)
+        total = 0
+        for epoch in range(cfg.epochs):
+            perm = epoch_permutation(cfg.seed, epoch, split).astype(np.int32)
+            perm_t.copy_(torch.from_numpy(perm))
+            counter.zero_()
+            metrics.zero_()
+            if use_graph and graph is None and steps > 1:
+                # warm one step eagerly (first-touch), then capture
+                step()
+                total += 1
+                s_ = torch.cuda.Stream(device=dev)
+                s_.wait_stream(torch.cuda.current_stream())
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s_):
+                    with torch.cuda.graph(graph, stream=s_):
+                        step()
+                torch.cuda.current_stream().wait_stream(s_)
+                remaining = steps - 1
+            else:
+                remaining = steps
+            for _ in range(remaining):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    step()
+                total += 1
+            m = metrics.cpu().numpy()
+            train_acc = m[:, 1] / np.maximum(m[:, 3], 1)
+            if cfg.val_every_epoch or epoch == cfg.epochs - 1:
+                val_acc, val_mse = self._evaluate_rows(dd["train_x"], dd["train_g"], dd["train_y"], split, n, cfg)
+        torch.cuda.synchronize(dev)
+        self._train_mem = mem
+        self.graph = graph
+        return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
+                         extra={"plan_s": self.timings["plan_s"], "launches_per_step": self.timings["launches_per_step"]})
+
+    # ---------------------------------------------------------------------------------------------
+    def export_arena(self, i: int, arena: torch.Tensor) -> Dict[int, Dict[str, np.ndarray]]:
+        """Export organism ``i``'s slice of an arena shaped like the parameters (e.g. gradients)."""
+        saved = self.p
+        try:
+            self.p = arena
+            out = self.export_params(i)
+        finally:
+            self.p = saved
+        return out
+
+    def debug_train_step(self, x: np.ndarray, g: np.ndarray, y: np.ndarray, apply_adam: bool = False):
+        """One training step on an explicit batch WITHOUT graph capture; returns (grad arena copy,
+        metrics).  Used by the numerics tests against the torch oracle."""
+        dev = self.device
+        B = len(x)
+        xb = torch.as_tensor(np.ascontiguousarray(x.reshape(B, -1)), dtype=torch.float32, device=dev).to(torch.bfloat16)
+        gb = torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32, device=dev).to(torch.bfloat16)
+        yb = torch.as_tensor(y.astype(np.int32), device=dev)
+        self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
+        metrics = torch.zeros(self.num_organisms, 4, dtype=torch.float32, device=dev)
+        mem = self._alloc_buffers(B, with_grads=True)
+        inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
+        plan = self._build_plan("train", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * self.num_organisms, metrics)
+        s = H.stream_handle()
+        self.g.zero_()
+        self.lib.memset32(mem["ws"].t.data_ptr(), mem["ws"].t.numel(), s)
+        fwd = Plan()
+        fwd.launches = plan.launches[:plan.fwd_count]
+        fwd.run()
+        self._run_loss(plan, True, B)
+        bwd = Plan()
+        bwd.launches = plan.launches[plan.fwd_count:]
+        bwd.run()
+        grads = self.g.clone()
+        if apply_adam:
+            c = self.cfg
+            self.lib.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
+                          self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), c.lr, c.beta1, c.beta2, c.eps, s)
+        torch.cuda.synchronize(dev)
+        self._debug_mem = mem
+        return grads, metrics.cpu().numpy()
+
+    def debug_logits(self, mem=None) -> List[np.ndarray]:
+        mem = mem or self._debug_mem
+        out = []
+        for i, lay in enumerate(self.layouts):
+            ir = lay.ir
+            NC, L = ir.num_classes, ir.genotype_size
+            kind, off = mem["orgs"][i]["act"][ir.cls_head]
+            out.append(mem["f32"].view(off, mem["B"] * (NC + L)).view(mem["B"], NC + L).cpu().numpy())
+        return out
+
+    # ---------------------------------------------------------------------------------------------
+    def _infer_plan(self, B):
+        key = ("infer", B)
+        if key not in self.plans:
+            dev = self.device
+            xcols = self.layouts[0].ir.nodes[0].shape[0] * self.layouts[0].ir.nodes[0].shape[1]
+            gcols = self.layouts[0].ir.genotype_size
+            xb = torch.zeros(B, xcols, dtype=torch.bfloat16, device=dev)
+            gb = torch.zeros(B, gcols, dtype=torch.bfloat16, device=dev)
+            yb = torch.zeros(B, dtype=torch.int32, device=dev)
+            metrics = torch.zeros(self.num_organisms, 4, dtype=torch.float32, device=dev)
+            self._input_tensors = getattr(self, "_input_tensors", {})
+            self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
+            mem = getattr(self, "_train_mem", None)
+            if mem is None or mem["B"] != B:
+                mem = self._alloc_buffers(B, with_grads=False)
+            inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
+            plan = self._build_plan("infer", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * self.num_organisms,
+                                    metrics)
+            self.plans[key] = (plan, xb, gb, yb, metrics, mem)
+        return self.plans[key]
+
+    def _evaluate_rows(self, X, G, Y, start, end, cfg):
+        P = self.num_organisms
+        n = end - start
+        if n <= 0:
+            return np.full(P, np.nan), np.full(P, np.nan)
+        B = cfg.batch_size
+        plan, xb, gb, yb, metrics, mem = self._infer_plan(B)
+        metrics.zero_()
+        perm = torch.arange(start, end, dtype=torch.int32, device=self.device)
+        L = self.lib
+        for base in range(0, n, B):
+            s = H.stream_handle()
+            L.gather_batch(X.data_ptr(), G.data_ptr(), Y.data_ptr(), perm.data_ptr(), 0, base, B, n, X.shape[1],
+                           G.shape[1], xb.data_ptr(), gb.data_ptr(), yb.data_ptr(), s)
+            plan.run()
+            self._run_loss(plan, False, min(B, n - base))
+        m = metrics.cpu().numpy()
+        return m[:, 1] / np.maximum(m[:, 3], 1), m[:, 2] / np.maximum(m[:, 3], 1)
+
+    def evaluate(self, x, labels, g, cfg: Optional[TrainConfig] = None) -> np.ndarray:
+        cfg = cfg or self.cfg
+        dd = device_data_for_arrays(x, labels, g, self.device)
+        acc, _ = self._evaluate_rows(dd["x"], dd["g"], dd["y"], 0, len(x), cfg)
+        return acc
+
+    def replicate(self, genotypes, images, cfg: Optional[TrainConfig] = None) -> List[np.ndarray]:
+        cfg = cfg or self.cfg
+        P = self.num_organisms
+        pool = len(images[0]) if P else 0
+        if pool == 0:
+            return [np.zeros((0, self.layouts[i].ir.genotype_size), np.float32) for i in range(P)]
+        outs = [[] for _ in range(P)]
+        B = min(pool, cfg.batch_size)
+        dev = self.device
+        for c0 in range(0, pool, B):
+            nb = min(B, pool - c0)
+            xs = torch.zeros(P, B, images[0][0].size, dtype=torch.bfloat16, device=dev)
+            gs = torch.zeros(P, B, self.layouts[0].ir.genotype_size, dtype=torch.bfloat16, device=dev)
+            xs[:, :nb] = torch.as_tensor(np.stack([im[c0:c0 + nb].reshape(nb, -1) for im in images]),
+                                         dtype=torch.float32, device=dev).to(torch.bfloat16)
+            gs[:, :nb] = torch.as_tensor(np.asarray(genotypes, np.float32), device=dev)[:, None, :].to(torch.bfloat16)
+            mem = self._alloc_buffers(B, with_grads=False) if not hasattr(self, "_rep_mem") or \
+                self._rep_mem["B"] != B else self._rep_mem
+            self._rep_mem = mem
+            self._input_tensors = getattr(self, "_input_tensors", {})
+            for i in range(P):
+                self._input_tensors[xs[i].data_ptr()] = xs[i]
+                self._input_tensors[gs[i].data_ptr()] = gs[i]
+            inputs = [{"X": xs[i].data_ptr(), "g": gs[i].data_ptr()} for i in range(P)]
+            plan = self._build_plan("infer", B, mem, inputs)
+            plan.run()
+            for i, lay in enumerate(self.layouts):
+                ir = lay.ir
+                NC, L = ir.num_classes, ir.genotype_size
+                kind, off = mem["orgs"][i]["act"][ir.cls_head]
+                logits = mem["f32"].view(off, B * (NC + L)).view(B, NC + L)
+                outs[i].append(torch.sigmoid(logits[:nb, NC:]).half().float().cpu().numpy())
+        return [np.concatenate(o, 0) for o in outs]
+
+    def close(self):
+        self.graph = None
+        self.plans.clear()
+
+
+def device_data_for_arrays(x, labels, g, device):
+    key = ("eval", id(x), str(device))
+    d = _DEVICE_DATA.get(key)
+    if d is None:
+        d = {"x": torch.as_tensor(np.ascontiguousarray(x.reshape(len(x), -1)), dtype=torch.float32).to(device).to(
+            torch.bfloat16),
+             "g": torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32).to(device).to(torch.bfloat16),
+             "y": torch.as_tensor(labels.astype(np.int32), device=device)}
+        _DEVICE_DATA[key] = d
+    return d

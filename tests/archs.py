@@ -1,0 +1,52 @@
+"""Architecture corpus for engine/kernel parity tests (decoded, no-space form and template form)."""
+
+ARCHS = {
+    "conv_pool_dense": (
+        "X_layer = Conv2D(filters=16, kernel_size=5, strides=1)(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=2)(X_layer)\n"
+        "X_layer = Dense(units=24, activation='relu')(X_layer)\n\n"
+        "g_layer = Dense(units=40, activation='sigmoid')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=64, activation='relu')(con)\n\nloss_balance = 0.7"),
+    "odd_channels_bn": (
+        "X_layer = Conv2D(filters=8, kernel_size=3, strides=2)(X_layer)\n"
+        "X_layer = Dense(units=13, activation='relu')(X_layer)\n"
+        "X_layer = BatchNormalization()(X_layer)\n"
+        "X_layer = Conv2D(filters=4, kernel_size=3, strides=1)(X_layer)\n\n"
+        "g_layer = Conv1D(filters=8, kernel_size=5, strides=2)(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=37, activation='sigmoid')(con)\ncon = BatchNormalization()(con)\n\nloss_balance = 0.3"),
+    "empty_x_branch": (
+        "g_layer = Dense(units=64, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=128, activation='relu')(con)\n\nloss_balance = 0.5"),
+    "bn_first_and_pool3": (
+        "X_layer = BatchNormalization()(X_layer)\n"
+        "X_layer = Conv2D(filters=32, kernel_size=7, strides=1)(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=3)(X_layer)\n\n"
+        "g_layer = Conv1D(filters=16, kernel_size=3, strides=1)(g_layer)\n"
+        "g_layer = Dense(units=9, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=48, activation='relu')(con)\ncon = Dense(units=32, activation='sigmoid')(con)\n\n"
+        "loss_balance = 0.9"),
+    "rewired_fanout": (
+        "X_layer = Conv2D(filters=8, kernel_size=5, strides=2)(X_layer)\n"
+        "g_layer = Dense(units=16, activation='relu')(g_layer)\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
+        "con = Dense(units=20, activation='relu')(con)\nloss_balance = 0.6"),
+    "mutant_neg_sub": (
+        "X_layer = Conv2D(filters=8, kernel_size=3, strides=2)(X_layer)\n"
+        "X_layer = -X_layer\n"
+        "g_layer = Dense(units=16, activation='relu')(g_layer)\n"
+        "g_layer = g_layer-1\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
+        "con = Dense(units=20, activation='relu')(con)\nloss_balance = 0.4"),
+    "conv1d_rank4_and_strided_pool": (
+        "X_layer = Conv2D(filters=8, kernel_size=3, strides=1)(X_layer)\n"
+        "X_layer = Conv1D(filters=8, kernel_size=3, strides=2)(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=3, strides=2)(X_layer)\n"
+        "g_layer = Conv1D(filters=3, kernel_size=1)(g_layer)\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
+        "con = Dense(units=24, activation='relu')(con)\nloss_balance = 0.5"),
+}

@@ -1,0 +1,155 @@
+"""HIP grouped engine vs. the torch fp32 oracle (same parameters, same batch).
+
+Numerics contract: bf16 operands / activations with fp32 accumulation and fp32 master weights, so
+forward logits and gradients are compared by relative Frobenius error.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from serann.genome.interpreter import interpret
+from serann.models.organism import Organism, init_params
+
+from .archs import ARCHS
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-12)
+
+
+def _batch(B, seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.random((B, 28, 28, 1)).astype(np.float32)
+    g = rng.integers(0, 2, (B, 100)).astype(np.float32)
+    y = rng.integers(0, 10, B).astype(np.int64)
+    return x, g, y
+
+
+def _oracle(ir, params, x, g, y):
+    dev = "cuda"
+    org = Organism(ir, params, device=dev)
+    xb = torch.as_tensor(x, device=dev)
+    gb = torch.as_tensor(g, device=dev)
+    yb = torch.as_tensor(y, device=dev)
+    cl, rl = org(xb, gb[..., None], training=True)
+    lb = ir.loss_balance
+    loss = lb * F.cross_entropy(cl, yb) + (1 - lb) * ((torch.sigmoid(rl) - gb) ** 2).mean()
+    loss.backward()
+    grads = {}
+    for k, p in org.params.items():
+        nid, name = k[1:].split("_", 1)
+        grads.setdefault(int(nid), {})[name] = p.grad.detach().cpu().numpy()
+    logits = torch.cat([cl, rl], 1).detach().cpu().numpy()
+    return logits, grads
+
+
+@pytest.mark.parametrize("name", sorted(ARCHS))
+def test_train_step_matches_oracle(name):
+    from serann.engine.hip_engine import HipPopulationEngine
+    ir = interpret(ARCHS[name])
+    params = init_params(ir, 7)
+    x, g, y = _batch(96)
+    eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    grads, metrics = eng.debug_train_step(x, g, y)
+    logits = eng.debug_logits()[0]
+    ref_logits, ref_grads = _oracle(ir, params, x, g, y)
+    assert _rel(logits, ref_logits) < 3e-2, _rel(logits, ref_logits)
+    hip_grads = eng.export_arena(0, grads)
+    for nid, d in ref_grads.items():
+        for k, v in d.items():
+            got = hip_grads[nid][k]
+            err = _rel(got, v)
+            assert err < 6e-2, (name, nid, k, err)
+    assert metrics[0, 3] == 96
+
+
+def test_population_grouping_matches_single():
+    """Grouping heterogeneous organisms into shared launches must not change any organism."""
+    from serann.engine.hip_engine import HipPopulationEngine
+    names = sorted(ARCHS)
+    irs = [interpret(ARCHS[n]) for n in names]
+    params = [init_params(ir, 11 + i) for i, ir in enumerate(irs)]
+    x, g, y = _batch(64, seed=3)
+    eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", params=params)
+    grads, _ = eng.debug_train_step(x, g, y)
+    logits = eng.debug_logits()
+    for i, ir in enumerate(irs):
+        single = HipPopulationEngine([ir], [0], device="cuda", params=[params[i]])
+        g1, _ = single.debug_train_step(x, g, y)
+        l1 = single.debug_logits()[0]
+        assert _rel(logits[i], l1) < 1e-6
+        a, b = eng.export_arena(i, grads), single.export_arena(0, g1)
+        for nid in b:
+            for k in b[nid]:
+                if k.startswith("moving"):
+                    continue
+                assert _rel(a[nid][k], b[nid][k]) < 1e-4, (names[i], nid, k)
+
+
+def test_fit_graph_replay_learns():
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=6000, n_test=1000, seed=5),
+                           n_train=6000, n_test=1000)
+    irs = [interpret(ARCHS[n]) for n in ("conv_pool_dense", "odd_channels_bn", "empty_x_branch")]
+    cfg = TrainConfig(epochs=2, batch_size=300)
+    eng = HipPopulationEngine(irs, [1, 2, 3], device="cuda", cfg=cfg)
+    res = eng.fit(data, cfg)
+    assert eng.graph is not None
+    assert res.steps == 2 * 19
+    assert np.all(np.isfinite(res.val_acc))
+    assert res.val_acc.mean() > 0.3, res.val_acc   # synthetic prototypes are easy
+    acc = eng.evaluate(data.test_x, data.test_labels, data.test_g, cfg)
+    assert np.all(acc > 0.2)
+    imgs = [data.test_x[:20]] * 3
+    outs = eng.replicate(np.ones((3, 100), np.float32), imgs, cfg)
+    assert outs[0].shape == (20, 100) and np.all((outs[0] >= 0) & (outs[0] <= 1))
+
+
+def test_adam_kernel_matches_keras_formula():
+    from serann.ops import hip_ops as H
+    lib = H.lib()
+    n = 1003
+    dev = "cuda"
+    torch.manual_seed(0)
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    pbf = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    lr_t = torch.zeros(1, device=dev)
+    p0, g0 = p.clone(), g.clone()
+    lib.adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pbf.data_ptr(), step.data_ptr(), lr_t.data_ptr(),
+             n, 1e-3, 0.9, 0.999, 1e-4, H.stream_handle())
+    torch.cuda.synchronize()
+    lr1 = 1e-3 * (1 - 0.999) ** 0.5 / (1 - 0.9)
+    m1 = 0.1 * g0
+    v1 = 0.001 * g0 * g0
+    ref = p0 - lr1 * m1 / (v1.sqrt() + 1e-4)
+    assert torch.allclose(p, ref, atol=1e-6, rtol=1e-5)
+    assert torch.all(g == 0)
+    assert int(step.item()) == 1
+    assert torch.allclose(pbf.float(), ref, atol=1e-2, rtol=1e-2)
+
+
+def test_popstats_kernel():
+    from serann.ops import hip_ops as H
+    from scipy.spatial.distance import pdist
+    rng = np.random.default_rng(0)
+    gen = rng.integers(0, 2, (300, 100)).astype(np.uint8)
+    bits = np.packbits(gen, axis=-1)
+    bits = np.pad(bits, ((0, 0), (0, 16 - bits.shape[1]))).view(np.uint64)
+    tb = torch.as_tensor(bits.view(np.int64), device="cuda")
+    out = torch.zeros(2, dtype=torch.float64, device="cuda")
+    H.lib().popstats(tb.data_ptr(), 300, 2, out.data_ptr(), H.stream_handle())
+    torch.cuda.synchronize()
+    sh, se = out.cpu().numpy()
+    npairs = 300 * 299 / 2
+    assert abs(sh / npairs / 100 - pdist(gen, "hamming").mean()) < 1e-9
+    assert abs(se / npairs - pdist(gen).mean()) < 1e-9
