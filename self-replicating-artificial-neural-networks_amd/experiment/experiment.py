@@ -224,9 +224,11 @@ class Experiment:
         local = [int(plan.trainable[i]) for i in parts[comm.rank]]
         ids = list(current.index)
         genotypes = np.stack([np.asarray(g, np.float64) for g in current["genotype"]])
+        position = {int(t): k for k, t in enumerate(plan.trainable)}
         res = self._worker.run(local, [ids[i] for i in local], genotypes[local] if local else genotypes[:0],
                                [plan.results[i].ir for i in local], int(pool_size), generation,
-                               self._random_seed)
+                               self._random_seed, positions=[position[i] for i in local],
+                               n_trainable=len(plan.trainable))
         payload = pack_results(res.indices, res.metrics, res.offspring, res.learning_time, res.replication_time)
         gathered = comm.allgather_bytes(payload)
 

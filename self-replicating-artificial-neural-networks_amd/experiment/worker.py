@@ -56,7 +56,11 @@ class ShardWorker:
                                             batch_size=int(parameters["training_batch_size"]))
 
     def run(self, indices: Sequence[int], ids: Sequence[str], genotypes: np.ndarray, irs: List[OrganismIR],
-            num_replications: int, generation: int, random_seed: int) -> ShardResult:
+            num_replications: int, generation: int, random_seed: int,
+            positions: Optional[Sequence[int]] = None, n_trainable: Optional[int] = None) -> ShardResult:
+        """``positions``/``n_trainable``: the organisms' positions among *all* trainable organisms of
+        the generation, which fixes their replication images independently of the partition (the
+        reference's single-job layout, experiment_worker.py:140-160)."""
         n = len(indices)
         L = int(self.params["genotype_size"])
         if n == 0:
@@ -76,9 +80,10 @@ class ShardWorker:
             replication_time = 0.0
             if num_replications > 0:
                 t0 = time.perf_counter()
-                total = n * num_replications
-                images = [d.test_x[replication_image_rows(p, num_replications, total, len(d.test_x))]
-                          for p in range(n)]
+                pos = list(range(n)) if positions is None else list(positions)
+                total = (n if n_trainable is None else n_trainable) * num_replications
+                images = [d.test_x[replication_image_rows(q, num_replications, total, len(d.test_x))]
+                          for q in pos]
                 outs = engine.replicate(np.asarray(genotypes, np.float32), images, cfg)
                 for p, o in enumerate(outs):
                     offspring[p] = np.round(np.clip(o, 0, 1)).astype(np.uint8)

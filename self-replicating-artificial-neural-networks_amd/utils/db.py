@@ -26,6 +26,14 @@ INT_COLUMNS = ["genotype_size", "initial_offspring_pool_size", "max_serann_param
 FLOAT_COLUMNS = ["error_correction_probability", "selection_pressure"]
 
 
+def _ts(v):
+    """Timestamps are stored as pandas writes datetime64 columns: 'YYYY-MM-DD HH:MM:SS.ffffff'."""
+    try:
+        return pd.Timestamp(v).strftime("%Y-%m-%d %H:%M:%S.%f")
+    except (TypeError, ValueError):
+        return v
+
+
 class ExperimentDB:
     def __init__(self, db_path, swallow_errors: bool = False):
         self._db_path = str(db_path)
@@ -55,7 +63,7 @@ class ExperimentDB:
 
     # ---- writers -------------------------------------------------------------------------------
     def save_execution_info(self, start_time, parameters: dict):
-        row = {"start_time": start_time}
+        row = {"start_time": _ts(start_time)}
         row.update(parameters)
         if "ancestor_genotype" in parameters and parameters["ancestor_genotype"] is not None:
             row["ancestor_genotype"] = "".join(str(int(i)) for i in row["ancestor_genotype"])
@@ -78,6 +86,7 @@ class ExperimentDB:
             df.to_sql("serann", conn, if_exists="append", index=True, index_label="id")
 
     def save_generation_info(self, generation_info: dict):
+        generation_info = {k: (_ts(v) if k == "start_time" else v) for k, v in generation_info.items()}
         with self.db_connection() as conn:
             pd.DataFrame([generation_info]).to_sql("generations", conn, index=False, if_exists="append")
 

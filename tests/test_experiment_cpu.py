@@ -1,0 +1,78 @@
+"""End-to-end generation loop on the CPU torch oracle (BASELINE config #1: pop=2, 1 generation),
+SQLite schema parity with the reference writer, and determinism / resume."""
+import sqlite3
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from serann.config import default_parameters
+from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+from serann.engine.base import TrainConfig
+from serann.experiment.experiment import Experiment
+from serann.experiment.worker import ShardWorker
+from serann.genome.codec import TableCodec
+from serann.utils.db import ExperimentDB
+
+SERANN_COLUMNS = ["id", "genotype", "source_code", "parent_id", "genotype_euclidean_distance_from_parent",
+                  "genotype_hamming_distance_from_parent", "source_code_levenshtein_distance_from_parent",
+                  "experiment_id", "generation", "num_offspring", "parameters_count", "loss_balance", "is_valid",
+                  "is_overweight", "classification_validation_accuracy", "classification_training_accuracy",
+                  "classification_test_accuracy", "replication_mse", "absolute_fertility", "relative_fertility",
+                  "classification_layers", "replication_layers", "merged_layers"]
+GEN_COLUMNS = ["experiment_id", "generation", "start_time", "survival_rate", "overweight_rate", "invalid_rate",
+               "mean_parameters_count", "mean_absolute_fertility", "absolute_fertility_std", "mean_loss_balance",
+               "mean_classification_validation_accuracy", "mean_classification_training_accuracy",
+               "mean_classification_test_accuracy", "max_classification_test_accuracy", "mean_replication_mse",
+               "learning_time_seconds", "replication_time_seconds", "total_time_seconds",
+               "mean_classification_layers", "mean_replication_layers", "mean_merged_layers",
+               "genotype_mean_pairwise_euclidean_distance", "genotype_mean_pairwise_hamming_distance",
+               "genotype_mean_euclidean_distance_from_parent", "genotype_mean_hamming_distance_from_parent",
+               "genotype_shannon_index", "genotype_nucleotide_diversity", "genotype_species_richness",
+               "source_code_median_levenshtein_distance_from_parent", "source_code_shannon_index",
+               "source_code_species_richness"]
+
+
+@pytest.fixture(scope="module")
+def small_data():
+    enc = synthetic_encodings()
+    return enc, get_serann_data(enc, synthetic_mnist(n_train=1200, n_test=300), n_train=1200, n_test=300)
+
+
+def _run(tmp_path, small_data, pop=2, gens=1, seed=5, name="e.sqlite"):
+    enc, data = small_data
+    p = default_parameters("example")
+    p.update(num_seranns=pop, num_generations=gens, training_epochs=1)
+    codec = TableCodec.from_generator(128, seed=1, ancestor=p["ancestor_genotype"])
+    w = ShardWorker(p, data, "torch", "cpu", TrainConfig(epochs=1, batch_size=200))
+    db = ExperimentDB(tmp_path / name)
+    e = Experiment("exp", enc, w, db, p, codec, random_seed=seed, verbose=False)
+    hist = e.execute()
+    return db, hist
+
+
+def test_pop2_one_generation_schema(tmp_path, small_data):
+    db, hist = _run(tmp_path, small_data)
+    con = sqlite3.connect(db.db_path)
+    serann = pd.read_sql("select * from serann", con)
+    gens = pd.read_sql("select * from generations", con)
+    info = pd.read_sql("select * from execution_info", con)
+    assert list(serann.columns) == SERANN_COLUMNS
+    assert list(gens.columns) == GEN_COLUMNS
+    assert len(serann) == 2 and len(gens) == 1 and len(info) == 1
+    assert serann["is_valid"].all()
+    assert serann["num_offspring"].sum() == 2
+    assert np.isclose(serann["relative_fertility"].sum(), 1.0)
+    assert serann["genotype"].iloc[0].startswith("[0, 0, 0")
+    assert info["ancestor_genotype"].iloc[0].startswith("0000000111")
+
+
+def test_multi_generation_determinism(tmp_path, small_data):
+    db1, h1 = _run(tmp_path, small_data, pop=4, gens=3, name="a.sqlite")
+    db2, h2 = _run(tmp_path, small_data, pop=4, gens=3, name="b.sqlite")
+    a = pd.read_sql("select id, genotype, source_code, num_offspring from serann", sqlite3.connect(db1.db_path))
+    b = pd.read_sql("select id, genotype, source_code, num_offspring from serann", sqlite3.connect(db2.db_path))
+    pd.testing.assert_frame_equal(a, b)
+    later = pd.read_sql("select * from serann where generation > 0", sqlite3.connect(db1.db_path))
+    assert later["parent_id"].notna().all()
+    assert later["genotype"].iloc[0].startswith("[0.0") or later["genotype"].iloc[0].startswith("[1.0")

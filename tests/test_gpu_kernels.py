@@ -1,0 +1,199 @@
+"""Per-kernel numerics on bf16-exact operands vs. plain PyTorch fp32 references of the same op.
+
+Operands are drawn as bf16 values, so the only differences are fp32 accumulation order and the
+final bf16 rounding of the output (<~0.4% relative)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from serann.ops import hip_ops as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def _desc(rows, dtype):
+    a = np.zeros(len(rows), dtype=dtype)
+    for i, r in enumerate(rows):
+        for k, v in r.items():
+            a[i][k] = v
+    return torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=DEV)
+
+
+def _run_gemm(mode, rows, dims):
+    d = _desc(rows, H.GEMM_DTYPE)
+    t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
+    H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    torch.cuda.synchronize()
+
+
+SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
+    (3, 28, 28, 1, 16, 5, 5, 1, 1, "relu"),
+    (2, 13, 13, 13, 4, 3, 3, 1, 1, "linear"),
+    (4, 12, 12, 16, 37, 3, 3, 2, 2, "sigmoid"),
+    (2, 9, 7, 64, 64, 1, 1, 1, 1, "relu"),
+    (5, 100, 1, 1, 32, 5, 1, 2, 1, "linear"),
+    (7, 1, 1, 868, 110, 1, 1, 1, 1, "linear"),
+    (2, 26, 26, 8, 8, 1, 3, 1, 2, "relu"),
+    (3, 10, 10, 24, 9, 7, 7, 1, 1, "linear"),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_grouped_conv_fwd_dgrad_wgrad(shape):
+    B, Hh, Ww, C, Fo, KH, KW, SH, SW, act = shape
+    OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16()   # Wm layout
+    bias = torch.randn(Fo, device=DEV, generator=g)
+    dz = torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = w.float().permute(0, 3, 1, 2)            # (F, C, KH, KW)
+    ref = F.conv2d(xr, wr, bias, (SH, SW)).permute(0, 2, 3, 1)
+    ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](ref)
+    # FWD
+    y = torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV)
+    K = KH * KW * C
+    flags = (H.GF_VEC_A if C % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)
+    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
+    _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=bias.data_ptr(),
+                                M=B * OH * OW, N=Fo, K=K, act=H.ACT_CODES[act], flags=flags, **geo)],
+              [(B * OH * OW, Fo, K)])
+    assert _rel(y.float(), ref) < 6e-3
+    # DGRAD
+    dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
+    ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    flags = (H.GF_VEC_A if Fo % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
+    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=w.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
+                                  K=KH * KW * Fo, flags=flags, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)])
+    assert _rel(dx.float(), ref_dx) < 6e-3
+    # WGRAD (accumulates into a zeroed fp32 buffer, split-K)
+    dw = torch.zeros(Fo, KH, KW, C, device=DEV)
+    ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
+                                  flags=flags, **geo)], [(Fo, K, B * OH * OW)])
+    assert _rel(dw, ref_dw) < 2e-5
+
+
+def test_grouped_gemm_many_problems_one_launch():
+    rows, dims, refs, outs = [], [], [], []
+    keep = []
+    for i, (B, Hh, Ww, C, Fo, KH, KW, SH, SW, act) in enumerate(SHAPES):
+        OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
+        x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
+        w = (torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16()
+        y = torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV)
+        keep += [x, w, y]
+        K = KH * KW * C
+        rows.append(dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH,
+                         KW=KW, SH=SH, SW=SW, M=B * OH * OW, N=Fo, K=K, act=0,
+                         flags=(H.GF_VEC_A if C % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)))
+        dims.append((B * OH * OW, Fo, K))
+        refs.append(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, (SH, SW)).permute(0, 2, 3, 1))
+        outs.append(y)
+    _run_gemm(H.MODE_FWD, rows, dims)
+    for y, r in zip(outs, refs):
+        assert _rel(y.float(), r) < 6e-3
+
+
+def test_bn_train_infer_backward():
+    R, C = 3000, 13
+    x = (torch.randn(R, C, device=DEV) * 3 + 1).bfloat16()
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV)
+    mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, invstd = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ws = torch.zeros(4 * C, device=DEV)
+    y = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
+    dy = torch.randn(R, C, device=DEV).bfloat16()
+    dx = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    row = dict(x=x.data_ptr(), y=y.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), gamma=gamma.data_ptr(),
+               beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(), invstd=invstd.data_ptr(),
+               ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
+    d = _desc([row], H.BN_DTYPE)
+    t = torch.as_tensor(H.chunk_tiles([R], H.BN_ROWS), device=DEV)
+    L, s = H.lib(), H.stream_handle()
+    for ph in (0, 1, 2):
+        L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
+    torch.cuda.synchronize()
+    xf = x.float().requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    mu, var = xf.mean(0), xf.var(0, unbiased=False)
+    ref = (xf - mu) / torch.sqrt(var + 1e-3) * g_ + b_
+    assert _rel(y.float(), ref.detach()) < 6e-3
+    assert torch.allclose(mm, 0.01 * mu.detach(), atol=1e-5)
+    assert torch.allclose(mv, 0.99 + 0.01 * var.detach() * R / (R - 1.001), atol=1e-4)
+    # backward (workspace re-zeroed, as the engine's per-step memset does)
+    ws.zero_()
+    for ph in (4, 5):
+        L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
+    torch.cuda.synchronize()
+    ref.backward(dy.float())
+    assert _rel(dx.float(), xf.grad) < 1e-2
+    assert _rel(dg, g_.grad) < 1e-3 and _rel(db, b_.grad) < 1e-3
+    # inference
+    L.bn(3, d.data_ptr(), t.data_ptr(), len(t), s)
+    torch.cuda.synchronize()
+    ref_inf = (x.float() - mm) / torch.sqrt(mv + 1e-3) * gamma + beta
+    assert _rel(y.float(), ref_inf) < 6e-3
+
+
+@pytest.mark.parametrize("p", [(2, 2, 2, 2), (3, 3, 3, 3), (3, 3, 2, 2), (2, 3, 1, 2)])
+def test_maxpool_fwd_bwd(p):
+    PH, PW, SH, SW = p
+    B, Hh, Ww, C = 3, 13, 11, 5
+    OH, OW = (Hh - PH) // SH + 1, (Ww - PW) // SW + 1
+    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
+    y = torch.zeros(B, OH, OW, C, dtype=torch.bfloat16, device=DEV)
+    idx = torch.zeros(B * OH * OW * C, dtype=torch.uint8, device=DEV)
+    dy = torch.randn(B, OH, OW, C, device=DEV).bfloat16()
+    dx = torch.zeros_like(x)
+    row = dict(x=x.data_ptr(), y=y.data_ptr(), idx=idx.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), B=B, H=Hh, W=Ww,
+               C=C, OH=OH, OW=OW, PH=PH, PW=PW, SH=SH, SW=SW, flags=0)
+    d = _desc([row], H.POOL_DTYPE)
+    L, s = H.lib(), H.stream_handle()
+    t = torch.as_tensor(H.chunk_tiles([B * OH * OW * C], H.POOL_ELEMS), device=DEV)
+    L.pool(0, d.data_ptr(), t.data_ptr(), len(t), s)
+    t2 = torch.as_tensor(H.chunk_tiles([B * Hh * Ww * C], H.POOL_ELEMS), device=DEV)
+    L.pool(1, d.data_ptr(), t2.data_ptr(), len(t2), s)
+    torch.cuda.synchronize()
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xf, (PH, PW), (SH, SW))
+    assert torch.equal(y.float(), ref.detach().permute(0, 2, 3, 1))
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dx.float(), xf.grad.permute(0, 2, 3, 1)) < 6e-3
+
+
+def test_loss_kernel_matches_keras_losses():
+    B, NC, L_ = 50, 10, 100
+    z = torch.randn(B, NC + L_, device=DEV)
+    labels = torch.randint(0, NC, (B,), device=DEV, dtype=torch.int32)
+    tgt = torch.randint(0, 2, (B, L_), device=DEV).bfloat16()
+    dz = torch.zeros(B, NC + L_, dtype=torch.bfloat16, device=DEV)
+    metrics = torch.zeros(4, device=DEV)
+    lb = 0.3
+    row = dict(logits=z.data_ptr(), dlogits=dz.data_ptr(), labels=labels.data_ptr(), target=tgt.data_ptr(),
+               metrics=metrics.data_ptr(), NC=NC, L=L_, B=B, lb=lb)
+    d = _desc([row], H.LOSS_DTYPE)
+    H.lib().loss(1, d.data_ptr(), 1, B, H.stream_handle(), B)
+    torch.cuda.synchronize()
+    zz = z.clone().requires_grad_(True)
+    ce = F.cross_entropy(zz[:, :NC], labels.long())
+    mse = ((torch.sigmoid(zz[:, NC:]) - tgt.float()) ** 2).mean()
+    loss = lb * ce + (1 - lb) * mse
+    loss.backward()
+    assert _rel(dz.float(), zz.grad) < 6e-3
+    assert abs(metrics[0].item() / B - loss.item()) < 1e-4
+    assert metrics[1].item() == (zz[:, :NC].argmax(1) == labels.long()).sum().item()
+    assert abs(metrics[2].item() / B - mse.item()) < 1e-5
