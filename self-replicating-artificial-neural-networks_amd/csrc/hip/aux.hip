@@ -37,156 +37,223 @@ __global__ void memset32_kernel(uint32_t* p, int64_t n) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// dz = dy * act'(y);  dbias += column sums of dz.   Chunk = 64 rows.
-constexpr int ACT_ROWS = 64;
-constexpr int SEG = 1024;
+// Channel-strided reduction layout shared by act_bwd and BatchNormalization (data [R][C] row-major):
+// a block owns a chunk of rows; for C <= 256 its 256 threads are arranged as (256/C) row lanes x C
+// channel lanes, so every thread keeps ONE channel for the whole chunk (parameters in registers, no
+// per-element division, no atomics in the loop); per-channel partials are combined through LDS and
+// leave the block as one global atomic per channel.  For C > 256 threads stride over channels.
+constexpr int RED_ELEMS = 16384;   // elements per block (chunk rows = max(1, RED_ELEMS / C))
 
+struct ChanMap {
+    int c0, cstride, rlane, rstride;   // first channel, channel step, first row offset, row step
+    bool active;
+};
+
+__device__ __forceinline__ ChanMap chan_map(int C) {
+    ChanMap m;
+    const int t = threadIdx.x;
+    if (C <= 256) {
+        const int rp = 256 / C;
+        m.c0 = t % C;
+        m.cstride = 1 << 30;          // one channel per thread
+        m.rlane = t / C;
+        m.rstride = rp;
+        m.active = t < rp * C;
+    } else {
+        m.c0 = t;
+        m.cstride = 256;
+        m.rlane = 0;
+        m.rstride = 1;
+        m.active = true;
+    }
+    return m;
+}
+
+__device__ __forceinline__ int chunk_rows(int C) { return max(1, RED_ELEMS / max(C, 1)); }
+
+// Reduce per-thread channel partials (v0, v1) for channel c0 (C <= 256 layout) into global ws.
+__device__ __forceinline__ void flush_partials(float* s0, float* s1, float v0, float v1, const ChanMap& m, int C,
+                                               float* g0, float* g1) {
+    const int t = threadIdx.x;
+    s0[t] = m.active ? v0 : 0.f;
+    if (g1) s1[t] = m.active ? v1 : 0.f;
+    __syncthreads();
+    if (t < C) {
+        float a = 0.f, b = 0.f;
+        for (int k = t; k < m.rstride * C; k += C) {
+            a += s0[k];
+            if (g1) b += s1[k];
+        }
+        atomicAdd(&g0[t], a);
+        if (g1) atomicAdd(&g1[t], b);
+    }
+    __syncthreads();
+}
+
+// dz = dy * act'(y);  dbias += column sums of dz.
 __global__ __launch_bounds__(256) void act_bwd_kernel(const ActBwdDesc* __restrict__ descs,
                                                       const int2* __restrict__ tiles) {
-    __shared__ float colsum[SEG];
+    __shared__ float s0[256];
     const int2 td = tiles[blockIdx.x];
     const ActBwdDesc& d = descs[td.x];
     const int M = (int)d.M, N = (int)d.N, act = (int)d.act;
     const bool write = d.flags & 1;
-    const bf16_t* dy = reinterpret_cast<const bf16_t*>(d.dy);
-    const bf16_t* y = reinterpret_cast<const bf16_t*>(d.y);
-    bf16_t* dz = reinterpret_cast<bf16_t*>(d.dz);
+    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+    const bf16_t* __restrict__ y = reinterpret_cast<const bf16_t*>(d.y);
+    bf16_t* __restrict__ dz = reinterpret_cast<bf16_t*>(d.dz);
     float* dbias = reinterpret_cast<float*>(d.dbias);
-    const int r0 = td.y * ACT_ROWS;
-    const int r1 = min(M, r0 + ACT_ROWS);
-    for (int seg = 0; seg < N; seg += SEG) {
-        const int sn = min(SEG, N - seg);
-        for (int i = threadIdx.x; i < sn; i += blockDim.x) colsum[i] = 0.f;
-        __syncthreads();
-        const int total = (r1 - r0) * sn;
-        for (int e = threadIdx.x; e < total; e += blockDim.x) {
-            const int r = r0 + e / sn, c = e % sn;
-            const int64_t off = (int64_t)r * N + seg + c;
-            float g = bf2f(dy[off]);
-            if (act != ACT_LINEAR) g *= act_grad_from_y(bf2f(y[off]), act);
-            if (write) dz[off] = f2bf(g);
-            if (dbias) atomicAdd(&colsum[c], g);
+    const int rows = chunk_rows(N);
+    const int r0 = td.y * rows, r1 = min(M, r0 + rows);
+    const ChanMap m = chan_map(N);
+    if (N <= 256) {
+        float acc = 0.f;
+        if (m.active) {
+            const int c = m.c0;
+            for (int r = r0 + m.rlane; r < r1; r += m.rstride) {
+                const int64_t off = (int64_t)r * N + c;
+                float g = bf2f(dy[off]);
+                if (act != ACT_LINEAR) g *= act_grad_from_y(bf2f(y[off]), act);
+                if (write) dz[off] = f2bf(g);
+                acc += g;
+            }
         }
-        __syncthreads();
-        if (dbias)
-            for (int i = threadIdx.x; i < sn; i += blockDim.x) atomicAdd(&dbias[seg + i], colsum[i]);
-        __syncthreads();
+        if (dbias) flush_partials(s0, nullptr, acc, 0.f, m, N, dbias, nullptr);
+    } else {
+        for (int c = m.c0; c < N; c += m.cstride) {
+            float acc = 0.f;
+            for (int r = r0; r < r1; ++r) {
+                const int64_t off = (int64_t)r * N + c;
+                float g = bf2f(dy[off]);
+                if (act != ACT_LINEAR) g *= act_grad_from_y(bf2f(y[off]), act);
+                if (write) dz[off] = f2bf(g);
+                acc += g;
+            }
+            if (dbias) atomicAdd(&dbias[c], acc);
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // BatchNormalizationF16 (channel-last, rows x C).  Phases:
-//   0: ws[c] += sum x            1: ws[C+c] += sum (x-mean)^2         2: train apply (+ moving stats)
-//   3: inference apply           4: ws2: sum dy, sum dy*xhat          5: backward apply (+ dgamma/dbeta)
-constexpr int BN_ROWS = 64;
+//   0: ws[c] += sum (x - K_c), ws[C+c] += sum (x - K_c)^2 with the shift K_c = x[0][c]
+//      (one pass, shifted sums keep the variance accurate when |mean| >> std)
+//   2: train apply (+ moving statistics, saved mean / invstd)      3: inference apply
+//   4: ws2[c] += sum dy, ws2[C+c] += sum dy*xhat                      5: backward apply (+ dgamma, dbeta)
+__device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const float* ws, int c, float& mu,
+                                         float& var) {
+    const float K = bf2f(reinterpret_cast<const bf16_t*>(d.x)[c]);
+    const float m1 = ws[c] / R;
+    mu = K + m1;
+    var = fmaxf(ws[C + c] / R - m1 * m1, 0.f);
+}
 
 __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ descs, const int2* __restrict__ tiles,
                                                  int phase) {
-    __shared__ float s0[SEG];
-    __shared__ float s1[SEG];
+    __shared__ float s0[256];
+    __shared__ float s1[256];
     const int2 td = tiles[blockIdx.x];
     const BnDesc& d = descs[td.x];
     const int R = (int)d.R, C = (int)d.C;
     const int flags = (int)d.flags;
     const float eps = (float)d.eps;
-    const bf16_t* x = reinterpret_cast<const bf16_t*>(d.x);
+    const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
     float* ws = reinterpret_cast<float*>(d.ws);
     const float* gamma = reinterpret_cast<const float*>(d.gamma);
     const float* beta = reinterpret_cast<const float*>(d.beta);
     float* mean = reinterpret_cast<float*>(d.mean);
     float* invstd = reinterpret_cast<float*>(d.invstd);
-    const int r0 = td.y * BN_ROWS, r1 = min(R, r0 + BN_ROWS);
-    const float invR = 1.f / (float)R;
+    const int rows = chunk_rows(C);
+    const int r0 = td.y * rows, r1 = min(R, r0 + rows);
+    const float Rf = (float)R;
+    const ChanMap m = chan_map(C);
 
-    if (phase == 0 || phase == 1 || phase == 4) {
-        for (int seg = 0; seg < C; seg += SEG) {
-            const int sn = min(SEG, C - seg);
-            for (int i = threadIdx.x; i < sn; i += blockDim.x) { s0[i] = 0.f; s1[i] = 0.f; }
-            __syncthreads();
-            const int total = (r1 - r0) * sn;
-            for (int e = threadIdx.x; e < total; e += blockDim.x) {
-                const int r = r0 + e / sn, c = e % sn, ch = seg + c;
-                const int64_t off = (int64_t)r * C + ch;
-                const float xv = bf2f(x[off]);
-                if (phase == 0) {
-                    atomicAdd(&s0[c], xv);
-                } else if (phase == 1) {
-                    const float dv = xv - ws[ch] * invR;
-                    atomicAdd(&s0[c], dv * dv);
-                } else {
-                    const float dyv = bf2f(reinterpret_cast<const bf16_t*>(d.dy)[off]);
-                    const float xh = (xv - mean[ch]) * invstd[ch];
-                    atomicAdd(&s0[c], dyv);
-                    atomicAdd(&s1[c], dyv * xh);
-                }
-            }
-            __syncthreads();
-            for (int i = threadIdx.x; i < sn; i += blockDim.x) {
-                if (phase == 0) atomicAdd(&ws[seg + i], s0[i]);
-                else if (phase == 1) atomicAdd(&ws[C + seg + i], s0[i]);
-                else { atomicAdd(&ws[seg + i], s0[i]); atomicAdd(&ws[C + seg + i], s1[i]); }
-            }
-            __syncthreads();
+    if (phase == 2 && td.y == 0) {
+        // moving averages (K.moving_average_update) and saved statistics, once per problem
+        const float mom = (float)d.momentum;
+        float* mm = reinterpret_cast<float*>(d.mm);
+        float* mv = reinterpret_cast<float*>(d.mv);
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            float mu, var;
+            bn_stats(d, C, Rf, ws, c, mu, var);
+            const float unbiased = var * (Rf / (Rf - (1.f + eps)));
+            mm[c] = mm[c] * mom + mu * (1.f - mom);
+            mv[c] = mv[c] * mom + unbiased * (1.f - mom);
+            mean[c] = mu;
+            invstd[c] = rsqrtf(var + eps);
         }
-        return;
     }
-    bf16_t* y = reinterpret_cast<bf16_t*>(d.y);
-    if (phase == 2 || phase == 3) {
-        if (phase == 2 && td.y == 0) {
-            // per-channel statistics, moving averages (K.moving_average_update), saved for backward
-            const float mom = (float)d.momentum;
-            float* mm = reinterpret_cast<float*>(d.mm);
-            float* mv = reinterpret_cast<float*>(d.mv);
-            for (int c = threadIdx.x; c < C; c += blockDim.x) {
-                const float mu = ws[c] * invR;
-                const float var = ws[C + c] * invR;
-                const float n = (float)R;
-                const float unbiased = var * (n / (n - (1.f + eps)));
-                mm[c] = mm[c] * mom + mu * (1.f - mom);
-                mv[c] = mv[c] * mom + unbiased * (1.f - mom);
+
+    for (int c = m.c0; c < C && m.active; c += m.cstride) {
+        const int rl = (C <= 256) ? m.rlane : 0, rs = (C <= 256) ? m.rstride : 1;
+        if (phase == 0) {
+            const float K = bf2f(x[c]);
+            float a = 0.f, b = 0.f;
+            for (int r = r0 + rl; r < r1; r += rs) {
+                const float v = bf2f(x[(int64_t)r * C + c]) - K;
+                a += v;
+                b += v * v;
             }
-        }
-        const int total = (r1 - r0) * C;
-        for (int e = threadIdx.x; e < total; e += blockDim.x) {
-            const int r = r0 + e / C, c = e % C;
-            const int64_t off = (int64_t)r * C + c;
+            if (C <= 256) { s0[threadIdx.x] = a; s1[threadIdx.x] = b; }
+            else { atomicAdd(&ws[c], a); atomicAdd(&ws[C + c], b); }
+        } else if (phase == 4) {
+            const float mu = mean[c], is = invstd[c];
+            const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+            float a = 0.f, b = 0.f;
+            for (int r = r0 + rl; r < r1; r += rs) {
+                const int64_t off = (int64_t)r * C + c;
+                const float g = bf2f(dy[off]);
+                a += g;
+                b += g * (bf2f(x[off]) - mu) * is;
+            }
+            if (C <= 256) { s0[threadIdx.x] = a; s1[threadIdx.x] = b; }
+            else { atomicAdd(&ws[c], a); atomicAdd(&ws[C + c], b); }
+        } else if (phase == 2 || phase == 3) {
             float mu, is;
             if (phase == 2) {
-                mu = ws[c] * invR;
-                is = rsqrtf(ws[C + c] * invR + eps);
-                if (td.y == 0 && r == r0) { mean[c] = mu; invstd[c] = is; }
+                float var;
+                bn_stats(d, C, Rf, ws, c, mu, var);
+                is = rsqrtf(var + eps);
             } else {
                 mu = reinterpret_cast<const float*>(d.mm)[c];
                 is = rsqrtf(reinterpret_cast<const float*>(d.mv)[c] + eps);
             }
-            float v = (bf2f(x[off]) - mu) * is;
-            if (flags & 1) v *= gamma[c];
-            if (flags & 2) v += beta[c];
-            y[off] = f2bf(v);
+            const float gsc = (flags & 1) ? gamma[c] * is : is;
+            const float sh = ((flags & 2) ? beta[c] : 0.f) - mu * gsc;
+            bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
+            for (int r = r0 + rl; r < r1; r += rs) {
+                const int64_t off = (int64_t)r * C + c;
+                y[off] = f2bf(bf2f(x[off]) * gsc + sh);
+            }
+        } else {   // phase 5
+            if (td.y == 0 && rl == 0) {
+                float* dg = reinterpret_cast<float*>(d.dgamma);
+                float* db = reinterpret_cast<float*>(d.dbeta);
+                if (flags & 1) dg[c] += ws[C + c];
+                if (flags & 2) db[c] += ws[c];
+            }
+            if (flags & 8) continue;
+            const float mu = mean[c], is = invstd[c];
+            const float gg = ((flags & 1) ? gamma[c] : 1.f) * is;
+            const float a = ws[c] / Rf, b = ws[C + c] / Rf;
+            const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+            bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
+            for (int r = r0 + rl; r < r1; r += rs) {
+                const int64_t off = (int64_t)r * C + c;
+                const float xh = (bf2f(x[off]) - mu) * is;
+                float v = gg * (bf2f(dy[off]) - a - xh * b);
+                if (flags & 4) v += bf2f(dx[off]);
+                dx[off] = f2bf(v);
+            }
         }
-        return;
     }
-    // phase 5: backward apply
-    if (td.y == 0) {
-        float* dg = reinterpret_cast<float*>(d.dgamma);
-        float* db = reinterpret_cast<float*>(d.dbeta);
-        for (int c = threadIdx.x; c < C; c += blockDim.x) {
-            if (flags & 1) dg[c] += ws[C + c];
-            if (flags & 2) db[c] += ws[c];
+    if ((phase == 0 || phase == 4) && C <= 256) {
+        __syncthreads();
+        if (threadIdx.x < C) {
+            float a = 0.f, b = 0.f;
+            for (int k = threadIdx.x; k < m.rstride * C; k += C) { a += s0[k]; b += s1[k]; }
+            atomicAdd(&ws[threadIdx.x], a);
+            atomicAdd(&ws[C + threadIdx.x], b);
         }
-    }
-    if (flags & 8) return;
-    const bf16_t* dy = reinterpret_cast<const bf16_t*>(d.dy);
-    bf16_t* dx = reinterpret_cast<bf16_t*>(d.dx);
-    const int total = (r1 - r0) * C;
-    for (int e = threadIdx.x; e < total; e += blockDim.x) {
-        const int r = r0 + e / C, c = e % C;
-        const int64_t off = (int64_t)r * C + c;
-        const float g = (flags & 1) ? gamma[c] : 1.f;
-        const float xh = (bf2f(x[off]) - mean[c]) * invstd[c];
-        float v = g * invstd[c] * (bf2f(dy[off]) - ws[c] * invR - xh * ws[C + c] * invR);
-        if (flags & 4) v += bf2f(dx[off]);
-        dx[off] = f2bf(v);
     }
 }
 
@@ -258,21 +325,40 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const PoolDesc* __restric
 }
 
 // ------------------------------------------------------------------------------------------------
-constexpr int COPY_ELEMS = 2048;
+constexpr int COPY_ROWS = 16;   // rows per block
 
 __global__ __launch_bounds__(256) void copy2d_kernel(const CopyDesc* __restrict__ descs, const int2* __restrict__ tiles) {
     const int2 td = tiles[blockIdx.x];
     const CopyDesc& d = descs[td.x];
-    const int64_t total = d.rows * d.cols;
-    const bf16_t* src = reinterpret_cast<const bf16_t*>(d.src);
-    bf16_t* dst = reinterpret_cast<bf16_t*>(d.dst);
-    const int64_t e0 = (int64_t)td.y * COPY_ELEMS;
-    for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + COPY_ELEMS); e += blockDim.x) {
-        const int64_t r = e / d.cols, c = e - r * d.cols;
-        float v = bf2f(src[r * d.src_stride + c]);
-        bf16_t* o = dst + r * d.dst_stride + c;
-        if (d.flags & 1) v += bf2f(*o);
-        *o = f2bf(v);
+    const bf16_t* __restrict__ src = reinterpret_cast<const bf16_t*>(d.src);
+    bf16_t* __restrict__ dst = reinterpret_cast<bf16_t*>(d.dst);
+    const int64_t cols = d.cols;
+    const bool acc = d.flags & 1;
+    const int64_t r0 = (int64_t)td.y * COPY_ROWS, r1 = min(d.rows, r0 + COPY_ROWS);
+    for (int64_t r = r0; r < r1; ++r) {
+        const bf16_t* s = src + r * d.src_stride;
+        bf16_t* o = dst + r * d.dst_stride;
+        // 16-B vectors (gfx950 serves them at any 2-B alignment), scalar tail
+        const int64_t nv = cols / 8;
+        for (int64_t v = threadIdx.x; v < nv; v += blockDim.x) {
+            uint4 val = *reinterpret_cast<const uint4*>(s + v * 8);
+            if (acc) {
+                uint4 old = *reinterpret_cast<const uint4*>(o + v * 8);
+                const bf16_t* a = reinterpret_cast<const bf16_t*>(&val);
+                const bf16_t* b = reinterpret_cast<const bf16_t*>(&old);
+                uint4 res;
+                bf16_t* c = reinterpret_cast<bf16_t*>(&res);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) c[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+                val = res;
+            }
+            *reinterpret_cast<uint4*>(o + v * 8) = val;
+        }
+        for (int64_t c = nv * 8 + threadIdx.x; c < cols; c += blockDim.x) {
+            float v = bf2f(s[c]);
+            if (acc) v += bf2f(o[c]);
+            o[c] = f2bf(v);
+        }
     }
 }
 
@@ -429,5 +515,35 @@ void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials,
     const unsigned t = (unsigned)((n + 63) / 64);
     hipLaunchKernelGGL(popstats_kernel, dim3(t, t), dim3(256), 0, as_stream(stream), as_ptr<const uint64_t>(bits),
                        (int)n, (int)words, as_ptr<double>(partials));
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// RiboAE decode epilogue: argmax over each group of V logits (K35).  One wave per group.
+__global__ __launch_bounds__(256) void group_argmax_kernel(const float* __restrict__ logits, int* __restrict__ out,
+                                                           int64_t ngroups, int V) {
+    const int64_t grp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (grp >= ngroups) return;
+    const int lane = threadIdx.x & 63;
+    const float* z = logits + grp * V;
+    float best = -INFINITY;
+    int bi = 1 << 30;
+    for (int v = lane; v < V; v += 64) {
+        const float x = z[v];
+        if (x > best) { best = x; bi = v; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == 0) out[grp] = bi;
+}
+
+void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream) {
+    if (ngroups <= 0) return;
+    hipLaunchKernelGGL(group_argmax_kernel, dim3((unsigned)((ngroups + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       as_ptr<const float>(logits), as_ptr<int>(out), ngroups, (int)V);
     SERANN_CHECK(hipGetLastError());
 }

@@ -15,6 +15,7 @@ static py::dict desc_sizes() {
     d["PoolDesc"] = sizeof(PoolDesc);
     d["CopyDesc"] = sizeof(CopyDesc);
     d["LossDesc"] = sizeof(LossDesc);
+    d["TransDesc"] = 5 * sizeof(int64_t);
     return d;
 }
 
@@ -23,6 +24,9 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("desc_sizes", &desc_sizes);
     m.def("grouped_gemm", &launch_grouped_gemm, py::arg("mode"), py::arg("descs"), py::arg("tiles"),
           py::arg("ntiles"), py::arg("stream"));
+    m.def("gemm2", &launch_gemm2, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
+          py::arg("ntiles"), py::arg("stream"));
+    m.def("transpose_weights", &launch_transpose_weights);
     m.def("adam", &launch_adam);
     m.def("f32_to_bf16", &launch_f32_to_bf16);
     m.def("gather_batch", &launch_gather_batch);
@@ -34,4 +38,5 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("loss", &launch_loss);
     m.def("popstats", &launch_popstats);
     m.def("memset32", &launch_memset32);
+    m.def("group_argmax", &launch_group_argmax);
 }

@@ -20,6 +20,8 @@ enum GemmFlags : int64_t {
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
 void launch_grouped_gemm(int mode, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_gemm2(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 
 // ---- optimizer --------------------------------------------------------------------------------
 void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
@@ -38,6 +40,7 @@ void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stre
 void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid);
 void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
+void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);
 
 // ---- auxiliary descriptors (int64 fields) ----------------------------------------------------
 struct ActBwdDesc { int64_t dy, y, dz, dbias, M, N, act, flags; };          // flags: 1 = write dz

@@ -33,7 +33,10 @@ from ..models.organism import glorot_limit, init_params
 from ..ops import hip_ops as H
 from .base import FitResult, PopulationEngine, TrainConfig, epoch_permutation
 
+import os
+
 ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp32
+GEMM_IMPL = os.environ.get("SERANN_GEMM", "v2")   # v2: direct-fragment FWD/DGRAD + tr-read WGRAD; v1: LDS tiles
 
 
 def _al(n: int) -> int:
@@ -124,6 +127,10 @@ class Plan:
             k = la.kind
             if k == "gemm":
                 L.grouped_gemm(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "gemm2":
+                L.gemm2(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "transpose":
+                L.transpose_weights(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "act_bwd":
                 L.act_bwd(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "bn":
@@ -184,6 +191,22 @@ class HipPopulationEngine(PopulationEngine):
             lay.w[ir.cls_head] = self.parena.alloc((NC + L) * D)
             lay.b[ir.cls_head] = self.parena.alloc(NC + L)
             self.layouts.append(lay)
+        # transposed bf16 weights for DGRAD (v2): Wt[C][KH][KW][F]
+        self.wt_off = []
+        wt_size = 0
+        for lay in self.layouts:
+            d = {}
+            for nid, off in lay.w.items():
+                n = lay.ir.node(nid)
+                a = n.attrs
+                if a["kind"] == "head_cls":
+                    cnt = (lay.ir.num_classes + lay.ir.genotype_size) * lay.ir.head_features
+                else:
+                    cnt = a["f"] * a["kh"] * a["kw"] * a["cin"]
+                d[nid] = wt_size
+                wt_size += _al(cnt)
+            self.wt_off.append(d)
+        self.wt = torch.zeros(max(wt_size, ALIGN), dtype=torch.bfloat16, device=dev)
         self.p = self.parena.materialize()
         self.g = torch.zeros_like(self.p)
         self.m = torch.zeros_like(self.p)
@@ -404,10 +427,27 @@ class HipPopulationEngine(PopulationEngine):
         def add_gemm(mode_, rows, dims):
             if not rows:
                 return
-            tiles = H.gemm_tiles(dims, mode_)
-            if len(tiles) == 0:
+            if GEMM_IMPL == "v1":
+                if mode_ == H.MODE_DGRAD:
+                    rows = [dict(r, b=r["b_v1"]) for r in rows]
+                rows = [{k: v for k, v in r.items() if k != "b_v1"} for r in rows]
+                tiles = H.gemm_tiles(dims, mode_)
+                if len(tiles):
+                    plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
                 return
-            plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
+            groups = {}
+            for r, dm in zip(rows, dims):
+                v = H.gemm2_variant(mode_, dm[0], dm[1])
+                groups.setdefault(v, ([], []))
+                groups[v][0].append({k: val for k, val in r.items() if k != "b_v1"})
+                groups[v][1].append(dm)
+            for v in sorted(groups):
+                rws, dms = groups[v]
+                bm, bn = H.gemm2_block(mode_, v)
+                tiles = H.gemm_tiles(dms, mode_, bm=bm, bn=bn)
+                if len(tiles):
+                    plan.launches.append(Launch("gemm2", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
+                                                len(tiles)))
 
         def add_chunked(kind, arg, rows, dtype, counts, chunk):
             if not rows:
@@ -491,7 +531,7 @@ class HipPopulationEngine(PopulationEngine):
                                             mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
                                             ws=mem["ws"].ptr(bd["ws"]), R=B * math.prod(n.shape) // c, C=c,
                                             flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
-                        bn_cnt.append(B * math.prod(n.shape) // c)
+                        bn_cnt.append(H.red_chunks(B * math.prod(n.shape) // c, c))
                     elif n.op == "concat":
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])
@@ -503,7 +543,7 @@ class HipPopulationEngine(PopulationEngine):
                             c_rows.append(dict(src=self._act_ptr(mem, o, i, inputs),
                                                dst=self._act_ptr(mem, o, n.id, inputs) + col * 2,
                                                rows=outer, cols=inner, src_stride=inner, dst_stride=out_inner))
-                            c_cnt.append(outer * inner)
+                            c_cnt.append(-(-outer // H.COPY_ROWS))
                             col += inner
                     else:
                         fallbacks.append((o, n))
@@ -511,12 +551,11 @@ class HipPopulationEngine(PopulationEngine):
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             if bn_rows:
                 if train:
-                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
-                    add_chunked("bn", 1, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
-                    add_chunked("bn", 2, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
+                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt, 1)
+                    add_chunked("bn", 2, bn_rows, H.BN_DTYPE, bn_cnt, 1)
                 else:
-                    add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, H.BN_ROWS)
-            add_chunked("copy", 0, c_rows, H.COPY_DTYPE, c_cnt, H.COPY_ELEMS)
+                    add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, 1)
+            add_chunked("copy", 0, c_rows, H.COPY_DTYPE, c_cnt, 1)
             for o, n in fallbacks:
                 plan.launches.append(Launch("fn", 0, None, None, 0, self._fallback_fwd(mem, o, n, inputs, B, train)))
 
@@ -551,6 +590,21 @@ class HipPopulationEngine(PopulationEngine):
             if not rec["req"].get(own, False):
                 return None
             return own
+
+        if GEMM_IMPL != "v1":
+            trows, tcnt = [], []
+            for o, lay in enumerate(self.layouts):
+                ir = lay.ir
+                for nid, off in lay.w.items():
+                    a = ir.node(nid).attrs
+                    if a["kind"] == "head_cls":
+                        F_, P_, C_ = ir.num_classes + ir.genotype_size, 1, ir.head_features
+                    else:
+                        F_, P_, C_ = a["f"], a["kh"] * a["kw"], a["cin"]
+                    trows.append(dict(src=wptr_bf(off), dst=self.wt.data_ptr() + 2 * self.wt_off[o][nid], F=F_, P=P_,
+                                      C=C_))
+                    tcnt.append(-(-(F_ * P_ * C_) // H.TRANS_ELEMS))
+            add_chunked("transpose", 0, trows, H.TRANS_DTYPE, tcnt, 1)
 
         STAGES = ("dgrad", "pool", "bn", "copy")
         for d in range(maxd, 0, -1):
@@ -590,7 +644,7 @@ class HipPopulationEngine(PopulationEngine):
                         if act != 0 or dbias:
                             ab_rows.append(dict(dy=dz, y=yv, dz=dz, dbias=dbias, M=M, N=F, act=act,
                                                 flags=1 if act != 0 else 0))
-                            ab_cnt.append(M)
+                            ab_cnt.append(H.red_chunks(M, F))
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
                         wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
@@ -599,7 +653,8 @@ class HipPopulationEngine(PopulationEngine):
                         own = target(o, n.inputs[0])
                         if own is not None:
                             Mi = B * Hh * Ww
-                            base = dict(a=dz, b=wptr_bf(lay.w[n.id]), out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
+                            base = dict(a=dz, b=self.wt.data_ptr() + 2 * self.wt_off[o][n.id], b_v1=wptr_bf(lay.w[n.id]),
+                                        out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
                                         W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,
                                         K=KH * KW * F)
                             tasks["dgrad"].append((o, own, lambda acc, r=base, v=vec: dict(r, flags=v | (H.GF_ACCUM if acc else 0)),
@@ -628,11 +683,13 @@ class HipPopulationEngine(PopulationEngine):
                                     dbeta=gptr(lay.beta[n.id]) if n.id in lay.beta else 0,
                                     R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
                         bn_red.append(dict(base, flags=pflags))
-                        bn_red_cnt.append(R)
+                        bn_red_cnt.append(H.red_chunks(R, c))
                         if own is None:
-                            tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8), R))
+                            tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
+                                                H.red_chunks(R, c)))
                         else:
-                            tasks["bn"].append((o, own, lambda acc, r=base, f=pflags: dict(r, flags=f | (4 if acc else 0)), R))
+                            tasks["bn"].append((o, own, lambda acc, r=base, f=pflags: dict(r, flags=f | (4 if acc else 0)),
+                                                H.red_chunks(R, c)))
                     elif n.op == "concat":
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])
@@ -646,14 +703,14 @@ class HipPopulationEngine(PopulationEngine):
                                 base = dict(src=dyp + col * 2, dst=mem["grad"].ptr(rec["grad"][own]), rows=outer,
                                             cols=inner, src_stride=out_inner, dst_stride=inner)
                                 tasks["copy"].append((o, own, lambda acc, r=base: dict(r, flags=1 if acc else 0),
-                                                      outer * inner))
+                                                      -(-outer // H.COPY_ROWS)))
                             col += inner
                     else:
                         fb.append((o, n))
-            add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, H.ACT_ROWS)
+            add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, 1)
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             if bn_red:
-                add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, H.BN_ROWS)
+                add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
             for stage in STAGES:
                 batches = [[]]
                 used = [set()]
@@ -677,9 +734,9 @@ class HipPopulationEngine(PopulationEngine):
                     elif stage == "pool":
                         add_chunked("pool", 1, rows, H.POOL_DTYPE, cnts, H.POOL_ELEMS)
                     elif stage == "bn":
-                        add_chunked("bn", 5, rows, H.BN_DTYPE, cnts, H.BN_ROWS)
+                        add_chunked("bn", 5, rows, H.BN_DTYPE, cnts, 1)
                     else:
-                        add_chunked("copy", 0, rows, H.COPY_DTYPE, cnts, H.COPY_ELEMS)
+                        add_chunked("copy", 0, rows, H.COPY_DTYPE, cnts, 1)
             for o, n in fb:
                 plan.launches.append(Launch("fn", 0, None, None, 0,
                                             self._fallback_bwd(mem, o, n, inputs, B, target, written)))

@@ -29,10 +29,15 @@ MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
 BM, BN, BK = 64, 64, 32
-ACT_ROWS = 64
-BN_ROWS = 64
+RED_ELEMS = 16384      # aux.hip: elements per block of the channel-strided reductions (BN, act_bwd)
 POOL_ELEMS = 1024
-COPY_ELEMS = 2048
+COPY_ROWS = 16
+
+
+def red_chunks(rows: int, channels: int) -> int:
+    """Blocks needed by a BN / act_bwd problem of shape [rows][channels]."""
+    per = max(1, RED_ELEMS // max(int(channels), 1))
+    return -(-int(rows) // per)
 
 
 def lib(required: bool = True):
@@ -53,7 +58,8 @@ def available() -> bool:
 def check_layouts():
     sizes = lib().desc_sizes()
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
-                     ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE)]:
+                     ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
+                     ("TransDesc", TRANS_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
@@ -70,11 +76,26 @@ def ptr(t) -> int:
 # ------------------------------------------------------------------------------------------------
 # tile tables
 # ------------------------------------------------------------------------------------------------
-def gemm_tiles(dims, mode: int, target_ksteps: int = 128, min_ksteps: int = 32) -> np.ndarray:
+TRANS_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "F", "P", "C"]])
+TRANS_ELEMS = 4096
+
+
+def gemm2_variant(mode: int, M: int, N: int) -> int:
+    """Tile variant of the v2 kernels: the column tile (FWD/DGRAD) or f tile (WGRAD) in {16, 32, 64}."""
+    dim = M if mode == MODE_WGRAD else N
+    return 16 if dim <= 16 else (32 if dim <= 32 else 64)
+
+
+def gemm2_block(mode: int, variant: int):
+    return (variant, 64) if mode == MODE_WGRAD else (128, variant)
+
+
+def gemm_tiles(dims, mode: int, target_ksteps: int = 128, min_ksteps: int = 32, bm: int = BM,
+               bn: int = BN) -> np.ndarray:
     """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16)."""
     rows = []
     for p, (M, N, K) in enumerate(dims):
-        tm, tn = -(-M // BM), -(-N // BN)
+        tm, tn = -(-M // bm), -(-N // bn)
         kt = -(-K // BK)
         if tm == 0 or tn == 0:
             continue

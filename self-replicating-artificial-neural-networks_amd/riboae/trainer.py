@@ -1,0 +1,132 @@
+"""RiboAE trainer (reference: ribosomal_autoencoder/training.py:25-133).
+
+Schedules (per batch number b, clamped to the schedule length):
+* temperature: logspace(log10(0.3), -3, 5e6)      (computed in closed form, not materialised)
+* learning rate: logspace(log10(3e-4), log10(2e-5), 1e6)
+* KL weight: linspace(0, 0.2, 1e7) ** 2
+Optimizer: Keras Adam (eps 1e-7) with the scheduled learning rate.  Batches are consumed in dataset
+order with ``repeat()`` semantics (no shuffle), batch 512.  Prints every 10 batches, a reconstruction
+every 50, and keeps only the most recent best-loss checkpoint at least ``min_backup_interval`` batches
+after the previous one -- plus (new) optimizer state + step so training can resume, bf16 autocast on
+MI355X, and an optional ``max_steps`` stop condition (the reference loop is infinite).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..engine.torch_engine import KerasAdam
+from ..models.riboae import ConcreteGAE
+from .io import save_checkpoint
+
+TEMPERATURE_STEPS = int(5e6)
+LEARNING_RATE_STEPS = int(1e6)
+KLD_STEPS = int(1e7)
+
+
+def _logspace_at(start, stop, n, i):
+    i = min(i, n - 1)
+    return 10 ** (start + (stop - start) * i / (n - 1))
+
+
+def temperature_at(b):
+    return _logspace_at(math.log10(0.3), -3.0, TEMPERATURE_STEPS, b)
+
+
+def learning_rate_at(b):
+    return _logspace_at(math.log10(3e-4), math.log10(2e-5), LEARNING_RATE_STEPS, b)
+
+
+def kld_weight_at(b):
+    b = min(b, KLD_STEPS - 1)
+    return (0.2 * b / (KLD_STEPS - 1)) ** 2
+
+
+class ScheduledKerasAdam(KerasAdam):
+    def step(self, lr: Optional[float] = None):
+        if lr is not None:
+            self.lr = lr
+        super().step()
+
+    def state_dict(self):
+        return {"t": self.t, "m": [m.detach().cpu() for m in self.m], "v": [v.detach().cpu() for v in self.v]}
+
+    def load_state_dict(self, st):
+        self.t = int(st["t"])
+        for dst, src in zip(self.m, st["m"]):
+            dst.copy_(src)
+        for dst, src in zip(self.v, st["v"]):
+            dst.copy_(src)
+
+
+def get_dataset(sequences: np.ndarray, train_test_ratio: float):
+    split = int(len(sequences) * train_test_ratio)
+    return sequences[:split], sequences[split:]
+
+
+def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out_dir: str, batch_size: int = 512,
+          min_backup_interval: int = 1000, max_steps: Optional[int] = None, device="cpu", log=print,
+          resume_path: Optional[str] = None, bf16: Optional[bool] = None, demo_every: int = 50, log_every: int = 10):
+    dev = torch.device(device)
+    model.to(dev).train()
+    opt = ScheduledKerasAdam(list(model.parameters()), lr=learning_rate_at(1), eps=1e-7)
+    start = 1
+    min_loss, min_loss_batch = float("inf"), 0
+    if resume_path:
+        ck = torch.load(resume_path, map_location=dev, weights_only=True)
+        model.load_state_dict(ck["state_dict"])
+        if ck.get("optimizer"):
+            opt.load_state_dict(ck["optimizer"])
+        start = int(ck["step"]) + 1
+        min_loss = float(ck.get("extra", {}).get("loss", min_loss))
+        min_loss_batch = int(ck["step"])
+    if bf16 is None:
+        bf16 = dev.type == "cuda"
+    data = torch.as_tensor(np.asarray(train_tokens), dtype=torch.long)
+    n = len(data)
+    nb = max(1, math.ceil(n / batch_size))
+    is_concrete = isinstance(model, ConcreteGAE)
+    history = []
+    b = start
+    t0 = time.perf_counter()
+    while max_steps is None or b < start + max_steps:
+        i = (b - 1) % nb
+        x = data[i * batch_size:(i + 1) * batch_size].to(dev, non_blocking=True)
+        temperature, lr, kw = temperature_at(b), learning_rate_at(b), kld_weight_at(b)
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bool(bf16)):
+            metrics = model.compute_loss(x, temperature, kw) if is_concrete else model.compute_loss(x)
+        opt.zero_grad()
+        metrics["loss"].float().backward()
+        opt.step(lr)
+        model._param_version = getattr(model, "_param_version", 0) + 1
+        loss = float(metrics["loss"].detach())
+        history.append(loss)
+        if b % log_every == 0:
+            log(f'Batch: {b} | Loss: {loss:.5f} | NLL: {float(metrics["nll"]):.5f} | KL: {float(metrics["kld"]):.5f} '
+                f'| {(time.perf_counter() - t0) / log_every * 1e3:.1f} ms/batch')
+            t0 = time.perf_counter()
+        if vocabulary is not None and demo_every and b % demo_every == 0:
+            model.eval()
+            with torch.no_grad():
+                z = model.encode(x[:1])
+                seq = model.decode(z).cpu().numpy()
+            model.train()
+            log(f"\n\nOriginal: \n{vocabulary.decode(x[:1].cpu().numpy())[0]}\n\n")
+            log(f"Genotype:\n{''.join(str(int(v)) for v in z[0].cpu().numpy())}\n\n")
+            log(f"Reconstruction: \n{vocabulary.decode(seq)[0]}\n\n")
+        if loss < min_loss and b - min_loss_batch >= min_backup_interval:
+            path = os.path.join(out_dir, f"{experiment_name}_b{b}.pt")
+            log("Backing up to: ", path)
+            save_checkpoint(path, model, "concrete" if is_concrete else "deterministic", b, opt.state_dict(),
+                            {"loss": loss})
+            prev = os.path.join(out_dir, f"{experiment_name}_b{min_loss_batch}.pt")
+            if min_loss_batch > 0 and os.path.exists(prev) and prev != path:
+                os.remove(prev)
+            min_loss, min_loss_batch = loss, b
+        b += 1
+    return history

@@ -28,10 +28,20 @@ def _desc(rows, dtype):
     return torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=DEV)
 
 
-def _run_gemm(mode, rows, dims):
-    d = _desc(rows, H.GEMM_DTYPE)
-    t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
-    H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+def _run_gemm(mode, rows, dims, impl="v1"):
+    if impl == "v1":
+        d = _desc(rows, H.GEMM_DTYPE)
+        t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
+        H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    else:
+        groups = {}
+        for r, dm in zip(rows, dims):
+            groups.setdefault(H.gemm2_variant(mode, dm[0], dm[1]), []).append((r, dm))
+        for v, items in groups.items():
+            d = _desc([r for r, _ in items], H.GEMM_DTYPE)
+            bm, bn = H.gemm2_block(mode, v)
+            t = torch.as_tensor(H.gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn), device=DEV)
+            H.lib().gemm2(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
     torch.cuda.synchronize()
 
 
@@ -47,8 +57,9 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
 ]
 
 
+@pytest.mark.parametrize("impl", ["v1", "v2"])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_grouped_conv_fwd_dgrad_wgrad(shape):
+def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     B, Hh, Ww, C, Fo, KH, KW, SH, SW, act = shape
     OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
     g = torch.Generator(device=DEV).manual_seed(0)
@@ -67,24 +78,37 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape):
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=bias.data_ptr(),
                                 M=B * OH * OW, N=Fo, K=K, act=H.ACT_CODES[act], flags=flags, **geo)],
-              [(B * OH * OW, Fo, K)])
+              [(B * OH * OW, Fo, K)], impl)
     assert _rel(y.float(), ref) < 6e-3
     # DGRAD
     dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
     ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     flags = (H.GF_VEC_A if Fo % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=w.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
-                                  K=KH * KW * Fo, flags=flags, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)])
+    wt = w.permute(3, 1, 2, 0).contiguous()       # Wt[C][KH][KW][F] for the v2 DGRAD kernel
+    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=(w if impl == "v1" else wt).data_ptr(), out=dx.data_ptr(),
+                                  M=B * Hh * Ww, N=C, K=KH * KW * Fo, flags=flags, **geo)],
+              [(B * Hh * Ww, C, KH * KW * Fo)], impl)
     assert _rel(dx.float(), ref_dx) < 6e-3
     # WGRAD (accumulates into a zeroed fp32 buffer, split-K)
     dw = torch.zeros(Fo, KH, KW, C, device=DEV)
     ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
-                                  flags=flags, **geo)], [(Fo, K, B * OH * OW)])
+                                  flags=flags, **geo)], [(Fo, K, B * OH * OW)], impl)
     assert _rel(dw, ref_dw) < 2e-5
 
 
-def test_grouped_gemm_many_problems_one_launch():
+def test_transpose_weights_kernel():
+    w = torch.randn(37, 3, 5, 13, device=DEV).bfloat16()
+    out = torch.zeros(13, 3, 5, 37, dtype=torch.bfloat16, device=DEV)
+    d = _desc([dict(src=w.data_ptr(), dst=out.data_ptr(), F=37, P=15, C=13)], H.TRANS_DTYPE)
+    t = torch.as_tensor(H.chunk_tiles([-(-w.numel() // H.TRANS_ELEMS)], 1), device=DEV)
+    H.lib().transpose_weights(d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(out, w.permute(3, 1, 2, 0).contiguous())
+
+
+@pytest.mark.parametrize("impl", ["v1", "v2"])
+def test_grouped_gemm_many_problems_one_launch(impl):
     rows, dims, refs, outs = [], [], [], []
     keep = []
     for i, (B, Hh, Ww, C, Fo, KH, KW, SH, SW, act) in enumerate(SHAPES):
@@ -100,7 +124,7 @@ def test_grouped_gemm_many_problems_one_launch():
         dims.append((B * OH * OW, Fo, K))
         refs.append(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, (SH, SW)).permute(0, 2, 3, 1))
         outs.append(y)
-    _run_gemm(H.MODE_FWD, rows, dims)
+    _run_gemm(H.MODE_FWD, rows, dims, impl)
     for y, r in zip(outs, refs):
         assert _rel(y.float(), r) < 6e-3
 
@@ -121,9 +145,9 @@ def test_bn_train_infer_backward():
                beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(), invstd=invstd.data_ptr(),
                ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
     d = _desc([row], H.BN_DTYPE)
-    t = torch.as_tensor(H.chunk_tiles([R], H.BN_ROWS), device=DEV)
+    t = torch.as_tensor(H.chunk_tiles([H.red_chunks(R, C)], 1), device=DEV)
     L, s = H.lib(), H.stream_handle()
-    for ph in (0, 1, 2):
+    for ph in (0, 2):
         L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
     torch.cuda.synchronize()
     xf = x.float().requires_grad_(True)
