@@ -129,4 +129,10 @@ def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out
                 os.remove(prev)
             min_loss, min_loss_batch = loss, b
         b += 1
+    if max_steps is not None and b - 1 != min_loss_batch:
+        # bounded runs always leave a final checkpoint (the reference loop never ends)
+        path = os.path.join(out_dir, f"{experiment_name}_b{b - 1}.pt")
+        save_checkpoint(path, model, "concrete" if is_concrete else "deterministic", b - 1, opt.state_dict(),
+                        {"loss": history[-1] if history else float("nan"), "final": True})
+        log("Final checkpoint: ", path)
     return history
