@@ -225,7 +225,7 @@ def prepare_muller_plot_data(df: pd.DataFrame, ancestor_id: Optional[str] = None
                 groups[key] = next_identity
                 next_identity += 1
             df.at[i, "identity"] = groups[key]
-    max_freq = df.groupby("identity").apply(lambda x: x.groupby("generation")["genotype"].count().max())
+    max_freq = df.groupby(["identity", "generation"])["genotype"].count().groupby(level=0).max()
     for parent_identity, off in df.sort_values("parent_identity", ascending=False).groupby("parent_identity", sort=False):
         cands = [parent_identity] + list(off["identity"].unique())
         max_freq.loc[parent_identity] = max(max_freq.reindex(cands).fillna(0))

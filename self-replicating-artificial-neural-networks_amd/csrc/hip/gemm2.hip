@@ -42,6 +42,23 @@ __device__ __forceinline__ G2 geo2(const GemmDesc& d) {
     return g;
 }
 
+// dZ = dY * act'(Y): the activation backward fused into the loads of the output gradient (the
+// separate act_bwd pass of v1 is gone); Y is the layer's post-activation output, same layout as dY.
+__device__ __forceinline__ uint4 act_grad8(uint4 dy, const bf16_t* __restrict__ y, int64_t off, int act, int n) {
+    if (act == ACT_LINEAR) return dy;
+    Frag g, yv, out;
+    g.u = dy;
+    if (n == 8) {
+        yv.u = *reinterpret_cast<const uint4*>(y + off);
+    } else {
+        yv.u = make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < n; ++j) yv.h[j] = y[off + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out.h[j] = f2bf(bf2f(g.h[j]) * act_grad_from_y(bf2f(yv.h[j]), act));
+    return out.u;
+}
+
 // ---- FWD A fragment: im2col row (pixel base `base`), reduction index k..k+7 -----------------------
 __device__ __forceinline__ uint4 fwd_a(const bf16_t* __restrict__ x, const G2& g, bool rowok, int base, int k) {
     Frag f;
@@ -68,8 +85,8 @@ __device__ __forceinline__ uint4 fwd_a(const bf16_t* __restrict__ x, const G2& g
 }
 
 // ---- DGRAD A fragment: dZ gathered at input pixel (b, ih, iw), k' = (kh*KW+kw)*F + f ------------------
-__device__ __forceinline__ uint4 dgrad_a(const bf16_t* __restrict__ dz, const G2& g, bool rowok, int b, int ih,
-                                         int iw, int k) {
+__device__ __forceinline__ uint4 dgrad_a(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ y, const G2& g,
+                                         bool rowok, int b, int ih, int iw, int k) {
     Frag fr;
     fr.u = make_uint4(0, 0, 0, 0);
     if (!rowok || k >= g.K) return fr.u;
@@ -81,8 +98,8 @@ __device__ __forceinline__ uint4 dgrad_a(const bf16_t* __restrict__ dz, const G2
         if (ohn < 0 || own < 0) return fr.u;
         const int oh = ohn / g.SH, ow = own / g.SW;
         if (oh * g.SH != ohn || ow * g.SW != own || oh >= g.OH || ow >= g.OW) return fr.u;
-        fr.u = *reinterpret_cast<const uint4*>(dz + ((b * g.OH + oh) * g.OW + ow) * g.F + f);
-        return fr.u;
+        const int64_t off = ((int64_t)(b * g.OH + oh) * g.OW + ow) * g.F + f;
+        return act_grad8(*reinterpret_cast<const uint4*>(dz + off), y, off, g.act, 8);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -95,7 +112,10 @@ __device__ __forceinline__ uint4 dgrad_a(const bf16_t* __restrict__ dz, const G2
         if (ohn < 0 || own < 0) continue;
         const int oh = ohn / g.SH, ow = own / g.SW;
         if (oh * g.SH != ohn || ow * g.SW != own || oh >= g.OH || ow >= g.OW) continue;
-        fr.h[j] = dz[((b * g.OH + oh) * g.OW + ow) * g.F + ff];
+        const int64_t off = ((int64_t)(b * g.OH + oh) * g.OW + ow) * g.F + ff;
+        float v = bf2f(dz[off]);
+        if (g.act != ACT_LINEAR) v *= act_grad_from_y(bf2f(y[off]), g.act);
+        fr.h[j] = f2bf(v);
     }
     return fr.u;
 }
@@ -119,17 +139,23 @@ __device__ __forceinline__ uint4 row_b(const bf16_t* __restrict__ w, int N, int 
 }  // namespace
 
 // ==================================================================================================
-// FWD / DGRAD direct kernel.  NT = BN / 16 column tiles per wave; block = 4 waves x 32 rows = 128 rows.
-template <int MODE, int NT>
+// FWD / DGRAD direct kernel.  NT = BN / 16 column tiles per wave.
+//   KW = false: block = 4 waves x 32 rows = 128 rows, every wave runs the whole k range.
+//   KW = true : block = 32 rows; the 4 waves split the k range (k-step w, w+4, ...) and their partial
+//               accumulators are summed through LDS -- for long-K / few-row problems (Dense on the
+//               flattened merge, heads) whose serial k loop would otherwise be latency-bound.
+template <int MODE, int NT, bool KW>
 __global__ __launch_bounds__(256) void gemm_direct_kernel(const GemmDesc* __restrict__ descs,
                                                           const int4* __restrict__ tiles) {
-    constexpr int BMB = 128, BNB = NT * 16;
+    constexpr int BMB = KW ? 32 : 128, BNB = NT * 16;
+    __shared__ float red[KW ? 3 * 2 * NT * 4 * 64 : 1];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G2 g = geo2(d);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, kg = (lane >> 4) * 8;
-    const int m_w = td.y * BMB + wave * 32;
+    const int m_w = td.y * BMB + (KW ? 0 : wave * 32);
+    const bf16_t* __restrict__ Yact = reinterpret_cast<const bf16_t*>(d.aux);
     const int n0 = td.z * BNB;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
     const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(d.a);
@@ -172,24 +198,48 @@ __global__ __launch_bounds__(256) void gemm_direct_kernel(const GemmDesc* __rest
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             fa[i].u = (MODE == MODE_FWD) ? fwd_a(A, g, rowok[i], base[i], k)
-                                         : dgrad_a(A, g, rowok[i], db[i], dih[i], diw[i], k);
+                                         : dgrad_a(A, Yact, g, rowok[i], db[i], dih[i], diw[i], k);
 #pragma unroll
         for (int j = 0; j < NT; ++j) fb[j].u = row_b(Bw, g.N, g.K, n0 + j * 16 + r16, k);
     };
 
-    if (kt0 < kt1) load(kt0);
-    for (int kt = kt0; kt < kt1; ++kt) {
+    const int kfirst = kt0 + (KW ? wave : 0), kstep = KW ? 4 : 1;
+    if (kfirst < kt1) load(kfirst);
+    for (int kt = kfirst; kt < kt1; kt += kstep) {
         Frag ca[2], cb[NT];
 #pragma unroll
         for (int i = 0; i < 2; ++i) ca[i] = fa[i];
 #pragma unroll
         for (int j = 0; j < NT; ++j) cb[j] = fb[j];
-        if (kt + 1 < kt1) load(kt + 1);
+        if (kt + kstep < kt1) load(kt + kstep);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[i].v, cb[j].v, acc[i][j], 0, 0, 0);
+    }
+    if (KW) {
+        // waves 1..3 park their partial sums in LDS, wave 0 reduces and runs the epilogue
+        if (wave > 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        red[((((wave - 1) * 2 + i) * NT + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (wave > 0) return;
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][j][r] += red[(((w * 2 + i) * NT + j) * 4 + r) * 64 + lane];
     }
 
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
@@ -238,6 +288,9 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
     const bf16_t* __restrict__ dZ = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
+    const bf16_t* __restrict__ Yact = reinterpret_cast<const bf16_t*>(d.aux);
+    float* __restrict__ dbias = reinterpret_cast<float*>(d.bias);
+    const bool has_bias = dbias != nullptr;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
 
     // wave layout: BMF=64 -> 2x2 waves of 32x32; BMF=32 -> 1x4 waves of 32x16; BMF=16 -> 1x4 of 16x16
@@ -262,14 +315,17 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
             const int m = m0 + a_m;
             const int f = f0 + a_f;
             if (m < g.K) {
-                const bf16_t* src = dZ + (int64_t)m * g.F + f;
-                if (f + 8 <= g.F) {
+                const int64_t off = (int64_t)m * g.F + f;
+                const bf16_t* src = dZ + off;
+                const int nv = min(8, g.F - f);
+                if (nv == 8) {
                     ra.u = *reinterpret_cast<const uint4*>(src);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if (f + j < g.F) ra.h[j] = src[j];
+                        if (j < nv) ra.h[j] = src[j];
                 }
+                ra.u = act_grad8(ra.u, Yact, off, g.act, nv);
             }
         }
         rb.u = make_uint4(0, 0, 0, 0);
@@ -283,6 +339,9 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
             G2 gg = g;
             gg.K = g.N;                                       // im2col width
             rb.u = fwd_a(X, gg, true, base, k0c + b_k);
+            // bias gradient = column of ones appended to im2col (column index N)
+            const int onecol = g.N - (k0c + b_k);
+            if (has_bias && onecol >= 0 && onecol < 8) rb.h[onecol] = (bf16_t)0x3F80;
         }
     };
     auto stash = [&]() {
@@ -342,11 +401,13 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
 #pragma unroll
         for (int j = 0; j < TK; ++j) {
             const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-            if (col >= g.N) continue;
+            if (col > g.N || (col == g.N && !has_bias)) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                if (row >= g.M) continue;
+                if (col < g.N) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                else atomicAdd(dbias + row, acc[i][j][r]);
             }
         }
 }
@@ -383,14 +444,22 @@ void launch_gemm2(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         if (variant == 16) hipLaunchKernelGGL(gemm_wgrad_kernel<16>, grid, block, 0, s, dp, tp);
         else if (variant == 32) hipLaunchKernelGGL(gemm_wgrad_kernel<32>, grid, block, 0, s, dp, tp);
         else hipLaunchKernelGGL(gemm_wgrad_kernel<64>, grid, block, 0, s, dp, tp);
-    } else if (mode == MODE_FWD) {
-        if (variant == 16) hipLaunchKernelGGL((gemm_direct_kernel<MODE_FWD, 1>), grid, block, 0, s, dp, tp);
-        else if (variant == 32) hipLaunchKernelGGL((gemm_direct_kernel<MODE_FWD, 2>), grid, block, 0, s, dp, tp);
-        else hipLaunchKernelGGL((gemm_direct_kernel<MODE_FWD, 4>), grid, block, 0, s, dp, tp);
     } else {
-        if (variant == 16) hipLaunchKernelGGL((gemm_direct_kernel<MODE_DGRAD, 1>), grid, block, 0, s, dp, tp);
-        else if (variant == 32) hipLaunchKernelGGL((gemm_direct_kernel<MODE_DGRAD, 2>), grid, block, 0, s, dp, tp);
-        else hipLaunchKernelGGL((gemm_direct_kernel<MODE_DGRAD, 4>), grid, block, 0, s, dp, tp);
+        const bool kw = variant >= 1000;
+        const int bn = variant % 1000;
+#define SERANN_DIRECT(M_, NT_, KW_) hipLaunchKernelGGL((gemm_direct_kernel<M_, NT_, KW_>), grid, block, 0, s, dp, tp)
+        if (mode == MODE_FWD) {
+            if (kw) { if (bn == 16) SERANN_DIRECT(MODE_FWD, 1, true); else if (bn == 32) SERANN_DIRECT(MODE_FWD, 2, true);
+                      else SERANN_DIRECT(MODE_FWD, 4, true); }
+            else    { if (bn == 16) SERANN_DIRECT(MODE_FWD, 1, false); else if (bn == 32) SERANN_DIRECT(MODE_FWD, 2, false);
+                      else SERANN_DIRECT(MODE_FWD, 4, false); }
+        } else {
+            if (kw) { if (bn == 16) SERANN_DIRECT(MODE_DGRAD, 1, true); else if (bn == 32) SERANN_DIRECT(MODE_DGRAD, 2, true);
+                      else SERANN_DIRECT(MODE_DGRAD, 4, true); }
+            else    { if (bn == 16) SERANN_DIRECT(MODE_DGRAD, 1, false); else if (bn == 32) SERANN_DIRECT(MODE_DGRAD, 2, false);
+                      else SERANN_DIRECT(MODE_DGRAD, 4, false); }
+        }
+#undef SERANN_DIRECT
     }
     SERANN_CHECK(hipGetLastError());
 }

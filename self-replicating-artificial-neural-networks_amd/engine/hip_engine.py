@@ -437,7 +437,7 @@ class HipPopulationEngine(PopulationEngine):
                 return
             groups = {}
             for r, dm in zip(rows, dims):
-                v = H.gemm2_variant(mode_, dm[0], dm[1])
+                v = H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
                 groups.setdefault(v, ([], []))
                 groups[v][0].append({k: val for k, val in r.items() if k != "b_v1"})
                 groups[v][1].append(dm)
@@ -641,19 +641,28 @@ class HipPopulationEngine(PopulationEngine):
                         M = B * OH * OW
                         K = KH * KW * C
                         dbias = gptr(lay.b[n.id]) if n.id in lay.b else 0
-                        if act != 0 or dbias:
+                        fused = GEMM_IMPL != "v1"
+                        if not fused and (act != 0 or dbias):
                             ab_rows.append(dict(dy=dz, y=yv, dz=dz, dbias=dbias, M=M, N=F, act=act,
                                                 flags=1 if act != 0 else 0))
                             ab_cnt.append(H.red_chunks(M, F))
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-                        wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
-                                            KH=KH, KW=KW, SH=SH, SW=SW, M=F, N=K, K=M, flags=vec))
-                        wg_dims.append((F, K, M))
+                        if fused:
+                            # v2: dZ = dY * act'(Y) on load, bias grad = extra ones-column of im2col
+                            wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), bias=dbias, aux=yv, act=act,
+                                                H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW,
+                                                M=F, N=K, K=M, flags=vec))
+                            wg_dims.append((F, K + (1 if dbias else 0), M))
+                        else:
+                            wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
+                                                KH=KH, KW=KW, SH=SH, SW=SW, M=F, N=K, K=M, flags=vec))
+                            wg_dims.append((F, K, M))
                         own = target(o, n.inputs[0])
                         if own is not None:
                             Mi = B * Hh * Ww
                             base = dict(a=dz, b=self.wt.data_ptr() + 2 * self.wt_off[o][n.id], b_v1=wptr_bf(lay.w[n.id]),
+                                        aux=yv if fused else 0, act=act if fused else 0,
                                         out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
                                         W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,
                                         K=KH * KW * F)

@@ -80,14 +80,20 @@ TRANS_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "F", "P", "C"]])
 TRANS_ELEMS = 4096
 
 
-def gemm2_variant(mode: int, M: int, N: int) -> int:
-    """Tile variant of the v2 kernels: the column tile (FWD/DGRAD) or f tile (WGRAD) in {16, 32, 64}."""
+def gemm2_variant(mode: int, M: int, N: int, K: int = 0) -> int:
+    """Tile variant of the v2 kernels: the column tile (FWD/DGRAD) or f tile (WGRAD) in {16, 32, 64};
+    FWD/DGRAD problems with few rows and a long k loop use the wave-split-K form (+1000)."""
     dim = M if mode == MODE_WGRAD else N
-    return 16 if dim <= 16 else (32 if dim <= 32 else 64)
+    v = 16 if dim <= 16 else (32 if dim <= 32 else 64)
+    if mode != MODE_WGRAD and M <= 8192 and -(-K // BK) >= 16:
+        v += 1000
+    return v
 
 
 def gemm2_block(mode: int, variant: int):
-    return (variant, 64) if mode == MODE_WGRAD else (128, variant)
+    if mode == MODE_WGRAD:
+        return (variant, 64)
+    return (32, variant % 1000) if variant >= 1000 else (128, variant)
 
 
 def gemm_tiles(dims, mode: int, target_ksteps: int = 128, min_ksteps: int = 32, bm: int = BM,

@@ -1,0 +1,94 @@
+"""Evaluation subsystem on CPU: samplers, SerannEvaluator (E replicas, R replications),
+SampleDeepEvaluator resume + pickle output, analysis loaders over the experiment DB."""
+import os
+import pickle
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from serann.analysis.results import (evaluations_from_pickle, genotype_to_hex, load_experiment_results,
+                                     prepare_muller_plot_data)
+from serann.config import default_parameters
+from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+from serann.engine.base import TrainConfig
+from serann.evaluation.driver import SAMPLERS, SampleDeepEvaluator
+from serann.evaluation.evaluator import SerannEvaluationWorker, probabilistic_proofreading
+from serann.experiment.experiment import Experiment
+from serann.experiment.worker import ShardWorker
+from serann.genome.codec import TableCodec
+from serann.utils.db import ExperimentDB
+
+
+@pytest.fixture(scope="module")
+def experiment(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("ev")
+    enc = synthetic_encodings()
+    data = get_serann_data(enc, synthetic_mnist(n_train=800, n_test=200), n_train=800, n_test=200)
+    p = default_parameters("example")
+    p.update(num_seranns=5, num_generations=3, training_epochs=1)
+    codec = TableCodec.from_generator(64, seed=1, ancestor=p["ancestor_genotype"])
+    w = ShardWorker(p, data, "torch", "cpu", TrainConfig(epochs=1, batch_size=200))
+    db = ExperimentDB(tmp / "exp.sqlite")
+    Experiment("exp", enc, w, db, p, codec, random_seed=2, verbose=False).execute()
+    df = load_experiment_results("exp_test_" + os.path.basename(str(tmp)), db_path=db.db_path, cache_invalidate=True)
+    return df, data, codec, p, tmp
+
+
+def test_results_loader_columns(experiment):
+    df, *_ = experiment
+    for c in ("genotype_hex", "is_mutant", "descendants", "parent_genotype_hex", "parent_generation"):
+        assert c in df.columns
+    assert (df[df["generation"] == 0]["parent_id"] == "experiment_ancestor_id").all()
+    assert genotype_to_hex([1, 0, 1]) == "0x5"
+
+
+@pytest.mark.parametrize("name", sorted(SAMPLERS))
+def test_samplers(experiment, name):
+    df, *_ = experiment
+    params = {"total_samples": 4, "generation_step": 1, "samples_per_generation": 1}
+    idx = SAMPLERS[name](seed=0).sample(df, params)
+    assert set(idx) <= set(df.index)
+
+
+def test_proofreading_reverts_fraction():
+    rng = np.random.RandomState(0)
+    parent = np.zeros(100)
+    off = np.ones((3, 100))
+    fixed = probabilistic_proofreading(parent, off, 0.5, rng)
+    assert (fixed != parent).sum() == 150
+    assert (probabilistic_proofreading(parent, off, 0.0, rng) == off).all()
+
+
+def test_evaluator_and_driver_resume(experiment, tmp_path):
+    df, data, codec, p, _ = experiment
+    ep = {k: p[k] for k in ("genotype_size", "error_correction_probability", "classification_image_dimensions",
+                            "num_classification_classes", "training_epochs", "training_batch_size")}
+    worker = SerannEvaluationWorker(ep, data, codec, num_evaluations=2, replications_per_evaluation=4, engine="torch",
+                                    device="cpu", train_cfg=TrainConfig(epochs=1, batch_size=200))
+    ids = list(df.index[:4])
+    out = tmp_path / "ev.pkl"
+    ev = SampleDeepEvaluator(df, str(out), ids, worker, batch=2, log=lambda *a, **k: None)
+    res = ev.run()
+    assert set(res) == set(ids)
+    valid = [i for i in ids if df.at[i, "is_valid"] and not df.at[i, "is_overweight"]]
+    for i in valid:
+        r = res[i]
+        assert len(r["classification_accuracy"]) == 2
+        assert len(r["mutation_rate"]) == 2 and sum(r["mutation_rate"][0].values()) == 4
+        assert sum(r["offspring_survival"][1].values()) == 4
+    with open(out, "rb") as f:
+        assert set(pickle.load(f)) == set(ids)
+    # resume: everything already evaluated -> nothing recomputed, backup written
+    ev2 = SampleDeepEvaluator(df, str(out), ids, worker, batch=2, log=lambda *a, **k: None)
+    assert ev2.run() == res
+    assert (tmp_path / "ev_backup.pkl").exists()
+    flat = evaluations_from_pickle(str(out))
+    assert set(flat["serann_id"]) == set(ids)
+
+
+def test_muller_plot_data(experiment):
+    df, *_ = experiment
+    pops, adj = prepare_muller_plot_data(df, frequency_threshold=0.0)
+    assert {"Generation", "Identity", "Population"} <= set(pops.columns)
+    assert (pops.groupby("Generation")["Population"].sum() == 5).all()

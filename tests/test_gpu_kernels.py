@@ -36,7 +36,7 @@ def _run_gemm(mode, rows, dims, impl="v1"):
     else:
         groups = {}
         for r, dm in zip(rows, dims):
-            groups.setdefault(H.gemm2_variant(mode, dm[0], dm[1]), []).append((r, dm))
+            groups.setdefault(H.gemm2_variant(mode, dm[0], dm[1], dm[2]), []).append((r, dm))
         for v, items in groups.items():
             d = _desc([r for r, _ in items], H.GEMM_DTYPE)
             bm, bn = H.gemm2_block(mode, v)
@@ -221,3 +221,51 @@ def test_loss_kernel_matches_keras_losses():
     assert abs(metrics[0].item() / B - loss.item()) < 1e-4
     assert metrics[1].item() == (zz[:, :NC].argmax(1) == labels.long()).sum().item()
     assert abs(metrics[2].item() / B - mse.item()) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid"])
+def test_v2_fused_act_grad_and_bias_grad(act):
+    """v2 WGRAD/DGRAD apply dZ = dY * act'(Y) on load and emit the bias gradient as an extra column."""
+    B, Hh, Ww, C, Fo, KH, KW, SH, SW = 3, 9, 9, 8, 13, 3, 3, 1, 1
+    OH, OW = Hh - 2, Ww - 2
+    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
+    w = (torch.randn(Fo, KH, KW, C, device=DEV) / 6).bfloat16()
+    ypre = torch.randn(B, OH, OW, Fo, device=DEV)
+    y = (torch.relu(ypre) if act == "relu" else torch.sigmoid(ypre)).bfloat16()
+    dy = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
+    yf = y.float()
+    dz = dy.float() * ((yf > 0).float() if act == "relu" else yf * (1 - yf))
+    dz = dz.bfloat16().float()
+    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
+    K = KH * KW * C
+    dw = torch.zeros(Fo, KH, KW, C, device=DEV)
+    db = torch.zeros(Fo, device=DEV)
+    _run_gemm(H.MODE_WGRAD, [dict(a=dy.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), bias=db.data_ptr(),
+                                  aux=y.data_ptr(), act=H.ACT_CODES[act], M=Fo, N=K, K=B * OH * OW, **geo)],
+              [(Fo, K + 1, B * OH * OW)], "v2")
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = w.float().permute(0, 3, 1, 2)
+    ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    assert _rel(dw, ref_dw) < 1e-3
+    assert _rel(db, dz.sum((0, 1, 2))) < 1e-3
+    dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), aux=y.data_ptr(),
+                                  act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
+              [(B * Hh * Ww, C, KH * KW * Fo)], "v2")
+    ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    assert _rel(dx.float(), ref_dx) < 6e-3
+
+
+def test_v2_wave_split_k_dense():
+    """Few rows, long K (the Dense-on-merge shape): the wave-split-K form must match."""
+    M, K, N = 750, 5003, 110
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 70).bfloat16()
+    b = torch.randn(N, device=DEV)
+    y = torch.zeros(M, N, device=DEV)
+    assert H.gemm2_variant(H.MODE_FWD, M, N, K) >= 1000
+    _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=1, W=1, C=K,
+                                OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=K, flags=H.GF_OUT_F32)],
+              [(M, N, K)], "v2")
+    assert _rel(y, x.float() @ w.float().t() + b) < 1e-4
