@@ -367,55 +367,65 @@ __global__ __launch_bounds__(256) void copy2d_kernel(const CopyDesc* __restrict_
 // replication logits), labels int [B], target bf16 [B][L].  Train: writes dlogits bf16 (d(lb*CE +
 // (1-lb)*MSE)/dz, Keras mean reduction over the batch) and accumulates metrics[0]+=loss,
 // metrics[1]+=correct, metrics[2]+=sum_row mean_j (sigmoid-g)^2, metrics[3]+=rows.
+constexpr int LOSS_ROWS = 64;   // rows per block (16 per wave); metrics reduced per block
+
 __global__ __launch_bounds__(256) void loss_kernel(const LossDesc* __restrict__ descs, int train, int nvalid) {
+    __shared__ float red[4][4];
     const LossDesc& d = descs[blockIdx.y];
     const int B = (int)d.B, NC = (int)d.NC, L = (int)d.L;
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= B) return;
-    const bool valid = train ? true : (row < nvalid);
-    const float* z = reinterpret_cast<const float*>(d.logits) + (int64_t)row * (NC + L);
-    const int label = reinterpret_cast<const int*>(d.labels)[row];
-    const bf16_t* tg = reinterpret_cast<const bf16_t*>(d.target) + (int64_t)row * L;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float lb = (float)d.lb;
     const float invB = 1.f / (float)B;
-    // --- softmax cross-entropy over NC <= 64 classes
-    float zc = lane < NC ? z[lane] : -INFINITY;
-    float mx = zc;
-    int amax = lane < NC ? lane : 1 << 30;
+    float m_loss = 0.f, m_corr = 0.f, m_sq = 0.f, m_n = 0.f;
+    const int r0 = blockIdx.x * LOSS_ROWS + wave * (LOSS_ROWS / 4);
+    for (int row = r0; row < min(B, r0 + LOSS_ROWS / 4); ++row) {
+        const bool valid = train ? true : (row < nvalid);
+        const float* z = reinterpret_cast<const float*>(d.logits) + (int64_t)row * (NC + L);
+        const int label = reinterpret_cast<const int*>(d.labels)[row];
+        const bf16_t* tg = reinterpret_cast<const bf16_t*>(d.target) + (int64_t)row * L;
+        // --- softmax cross-entropy over NC <= 64 classes
+        const float zc = lane < NC ? z[lane] : -INFINITY;
+        float mx = zc;
+        int amax = lane < NC ? lane : 1 << 30;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float om = __shfl_xor(mx, o, 64);
-        const int oi = __shfl_xor(amax, o, 64);
-        if (om > mx || (om == mx && oi < amax)) { mx = om; amax = oi; }
-    }
-    const float ex = lane < NC ? __expf(zc - mx) : 0.f;
-    const float se = warp_sum(ex);
-    const float zl = __shfl(zc, label < 64 ? label : 0, 64);
-    const float ce = (__logf(se) + mx) - zl;
-    // --- sigmoid MSE over L replication outputs
-    float sq = 0.f;
-    for (int j = lane; j < L; j += 64) {
-        const float s = 1.f / (1.f + __expf(-z[NC + j]));
-        const float err = s - bf2f(tg[j]);
-        sq += err * err;
-        if (train) {
-            const float gr = (1.f - lb) * invB * 2.f * err / (float)L * s * (1.f - s);
-            reinterpret_cast<bf16_t*>(d.dlogits)[(int64_t)row * (NC + L) + NC + j] = f2bf(gr);
+        for (int o = 32; o > 0; o >>= 1) {
+            const float om = __shfl_xor(mx, o, 64);
+            const int oi = __shfl_xor(amax, o, 64);
+            if (om > mx || (om == mx && oi < amax)) { mx = om; amax = oi; }
+        }
+        const float ex = lane < NC ? __expf(zc - mx) : 0.f;
+        const float se = warp_sum(ex);
+        const float zl = __shfl(zc, label < 64 ? label : 0, 64);
+        const float ce = (__logf(se) + mx) - zl;
+        // --- sigmoid MSE over L replication outputs
+        float sq = 0.f;
+        for (int j = lane; j < L; j += 64) {
+            const float sg = 1.f / (1.f + __expf(-z[NC + j]));
+            const float err = sg - bf2f(tg[j]);
+            sq += err * err;
+            if (train) {
+                const float gr = (1.f - lb) * invB * 2.f * err / (float)L * sg * (1.f - sg);
+                reinterpret_cast<bf16_t*>(d.dlogits)[(int64_t)row * (NC + L) + NC + j] = f2bf(gr);
+            }
+        }
+        sq = warp_sum(sq);
+        if (train && lane < NC) {
+            const float p = ex / se;
+            const float gc = lb * invB * (p - (lane == label ? 1.f : 0.f));
+            reinterpret_cast<bf16_t*>(d.dlogits)[(int64_t)row * (NC + L) + lane] = f2bf(gc);
+        }
+        if (valid) {
+            m_loss += lb * ce + (1.f - lb) * sq / (float)L;
+            m_corr += amax == label ? 1.f : 0.f;
+            m_sq += sq / (float)L;
+            m_n += 1.f;
         }
     }
-    sq = warp_sum(sq);
-    if (train && lane < NC) {
-        const float p = ex / se;
-        const float gc = lb * invB * (p - (lane == label ? 1.f : 0.f));
-        reinterpret_cast<bf16_t*>(d.dlogits)[(int64_t)row * (NC + L) + lane] = f2bf(gc);
-    }
-    if (lane == 0 && valid) {
-        float* m = reinterpret_cast<float*>(d.metrics);
-        atomicAdd(&m[0], lb * ce + (1.f - lb) * sq / (float)L);
-        atomicAdd(&m[1], amax == label ? 1.f : 0.f);
-        atomicAdd(&m[2], sq / (float)L);
-        atomicAdd(&m[3], 1.f);
+    if (lane == 0) { red[wave][0] = m_loss; red[wave][1] = m_corr; red[wave][2] = m_sq; red[wave][3] = m_n; }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        if (v != 0.f) atomicAdd(reinterpret_cast<float*>(d.metrics) + threadIdx.x, v);
     }
 }
 
@@ -504,7 +514,7 @@ void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stre
 
 void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid) {
     if (nprob <= 0 || B <= 0) return;
-    dim3 grid((unsigned)((B + 3) / 4), (unsigned)nprob);
+    dim3 grid((unsigned)((B + LOSS_ROWS - 1) / LOSS_ROWS), (unsigned)nprob);
     hipLaunchKernelGGL(loss_kernel, grid, dim3(256), 0, as_stream(stream), as_ptr<const LossDesc>(descs), train,
                        (int)nvalid);
     SERANN_CHECK(hipGetLastError());
@@ -545,5 +555,52 @@ void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t
     if (ngroups <= 0) return;
     hipLaunchKernelGGL(group_argmax_kernel, dim3((unsigned)((ngroups + 3) / 4)), dim3(256), 0, as_stream(stream),
                        as_ptr<const float>(logits), as_ptr<int>(out), ngroups, (int)V);
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Shared im2col of a single-channel network input (MNIST image X or genotype g) for one
+// (KH, KW, SH, SW) configuration: out[m][k] (row stride K8 = roundup(KH*KW, 8), zero padded).
+// Every organism of the population reads the SAME input batch, so the first-layer convolutions of
+// all organisms with this configuration share one materialised im2col matrix, which turns their
+// forward and weight-gradient GEMMs into aligned 16-B-vector 1x1 problems.
+constexpr int IMCOL_ROWS = 64;
+
+__global__ __launch_bounds__(256) void imcol_kernel(const ImcolDesc* __restrict__ descs, const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const ImcolDesc& d = descs[td.x];
+    const int H = (int)d.H, W = (int)d.W, OH = (int)d.OH, OW = (int)d.OW, KW = (int)d.KW, KH = (int)d.KH;
+    const int SH = (int)d.SH, SW = (int)d.SW, K8 = (int)d.K8, K = KH * KW;
+    const int64_t M = d.B * OH * OW;
+    const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
+    bf16_t* __restrict__ out = reinterpret_cast<bf16_t*>(d.out);
+    const int chunks = K8 / 8;
+    const int64_t m0 = (int64_t)td.y * IMCOL_ROWS;
+    for (int e = threadIdx.x; e < IMCOL_ROWS * chunks; e += blockDim.x) {
+        const int64_t m = m0 + e / chunks;
+        if (m >= M) break;
+        const int c8 = (e % chunks) * 8;
+        const int64_t b = m / (OH * OW);
+        const int r = (int)(m - b * OH * OW);
+        const int oh = r / OW, ow = r - (r / OW) * OW;
+        const bf16_t* src = x + (b * H + oh * SH) * W + ow * SW;
+        union { uint4 u; bf16_t h[8]; } v;
+        v.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = c8 + j;
+            if (k < K) {
+                const int kh = k / KW, kw = k - (k / KW) * KW;
+                v.h[j] = src[kh * W + kw];
+            }
+        }
+        *reinterpret_cast<uint4*>(out + m * K8 + c8) = v.u;
+    }
+}
+
+void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipLaunchKernelGGL(imcol_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
+                       as_ptr<const ImcolDesc>(descs), as_ptr<const int2>(tiles));
     SERANN_CHECK(hipGetLastError());
 }

@@ -339,9 +339,6 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
             G2 gg = g;
             gg.K = g.N;                                       // im2col width
             rb.u = fwd_a(X, gg, true, base, k0c + b_k);
-            // bias gradient = column of ones appended to im2col (column index N)
-            const int onecol = g.N - (k0c + b_k);
-            if (has_bias && onecol >= 0 && onecol < 8) rb.h[onecol] = (bf16_t)0x3F80;
         }
     };
     auto stash = [&]() {
@@ -358,10 +355,20 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
     // transposing-read addressing: lane = 16*grp + 4*q + p supplies row (mrow + q), col (col0 + 4p)
     const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
 
+    // bias gradient: sum_m dZ[m][f], accumulated from the A tiles by the blocks of k-column tile 0
+    const bool do_bias = has_bias && td.z == 0;
+    float bsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+
     if (kt0 < kt1) load(kt0);
     for (int kt = kt0; kt < kt1; ++kt) {
         __syncthreads();
         stash();
+        if (do_bias) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += bf2f(ra.h[j]);
+        }
         __syncthreads();
         if (kt + 1 < kt1) load(kt + 1);
         Frag fa[TF], fbk[TK];
@@ -394,6 +401,18 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fbk[j].v, acc[i][j], 0, 0, 0);
     }
 
+    if (do_bias) {
+        // lanes of one wave holding the same f chunk differ in the bits >= log2(ACH): butterfly-reduce them
+#pragma unroll
+        for (int xo = ACH; xo < 64; xo <<= 1)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
+        if (a_act && lane < ACH) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (f0 + a_f + j < g.F) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+        }
+    }
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     float* out = reinterpret_cast<float*>(d.out);
 #pragma unroll
@@ -401,13 +420,11 @@ __global__ __launch_bounds__(256) void gemm_wgrad_kernel(const GemmDesc* __restr
 #pragma unroll
         for (int j = 0; j < TK; ++j) {
             const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-            if (col > g.N || (col == g.N && !has_bias)) continue;
+            if (col >= g.N) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row >= g.M) continue;
-                if (col < g.N) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
-                else atomicAdd(dbias + row, acc[i][j][r]);
+                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
             }
         }
 }

@@ -16,6 +16,7 @@ static py::dict desc_sizes() {
     d["CopyDesc"] = sizeof(CopyDesc);
     d["LossDesc"] = sizeof(LossDesc);
     d["TransDesc"] = 5 * sizeof(int64_t);
+    d["ImcolDesc"] = sizeof(ImcolDesc);
     return d;
 }
 
@@ -39,4 +40,5 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("popstats", &launch_popstats);
     m.def("memset32", &launch_memset32);
     m.def("group_argmax", &launch_group_argmax);
+    m.def("imcol", &launch_imcol);
 }

@@ -40,6 +40,7 @@ void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stre
 void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid);
 void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
+void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);
 
 // ---- auxiliary descriptors (int64 fields) ----------------------------------------------------
@@ -51,6 +52,7 @@ struct BnDesc {
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
 struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
+struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;
     double lb;

@@ -131,6 +131,8 @@ class Plan:
                 L.gemm2(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "transpose":
                 L.transpose_weights(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "imcol":
+                L.imcol(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "act_bwd":
                 L.act_bwd(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "bn":
@@ -473,6 +475,34 @@ class HipPopulationEngine(PopulationEngine):
 
         f32a = mem["f32"]
 
+        # Shared im2col of the raw inputs: when every organism reads the same input batch, all
+        # first-layer convolutions with the same (KH, KW, SH, SW) share one materialised im2col
+        # matrix, and their FWD / WGRAD become aligned 1x1 problems (v2 only).
+        shared_inputs = GEMM_IMPL != "v1" and all(inp == inputs[0] for inp in inputs)
+        imcol: Dict[tuple, dict] = {}
+
+        def raw_conv_imcol(o, n):
+            if not shared_inputs:
+                return None
+            a = n.attrs
+            ir_ = self.layouts[o].ir
+            src = ir_.node(mem["orgs"][o]["owner"][n.inputs[0]])
+            if src.op != "input" or a["kh"] * a["kw"] == 1 or a["kind"] not in ("conv2d", "conv1d") or a["cin"] != 1:
+                return None
+            key = (src.attrs["name"], a["h"], a["w"], a["kh"], a["kw"], a["sh"], a["sw"])
+            if key not in imcol:
+                k8 = -(-(a["kh"] * a["kw"]) // 8) * 8
+                rows = B * a["oh"] * a["ow"]
+                buf = torch.zeros(rows * k8 + 8, dtype=torch.bfloat16, device=self.device)
+                plan.keep.append(buf)
+                imcol[key] = dict(buf=buf, K8=k8, rows=rows,
+                                  desc=dict(x=inputs[0][src.attrs["name"]], out=buf.data_ptr(), B=B, H=a["h"], W=a["w"],
+                                            OH=a["oh"], OW=a["ow"], KH=a["kh"], KW=a["kw"], SH=a["sh"], SW=a["sw"],
+                                            K8=k8))
+            return imcol[key]
+
+        plan.imcol_lookup = raw_conv_imcol
+
         # ---- forward ---------------------------------------------------------------------------
         for d in range(1, maxd + 1):
             g_rows, g_dims = [], []
@@ -509,9 +539,15 @@ class HipPopulationEngine(PopulationEngine):
                         if K % 8 == 0:
                             flags |= H.GF_VEC_B
                         bias = pptr(lay.b[n.id]) if n.id in lay.b else 0
-                        g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
-                                           OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
-                                           flags=flags))
+                        ic = raw_conv_imcol(o, n) if a["kind"] != "head_cls" else None
+                        if ic is not None:
+                            g_rows.append(dict(a=ic["buf"].data_ptr(), b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=OH,
+                                               W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=F,
+                                               K=K, act=act, flags=flags))
+                        else:
+                            g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
+                                               OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
+                                               flags=flags))
                         g_dims.append((M, F, K))
                     elif n.op == "pool":
                         p_rows.append(dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
@@ -558,6 +594,12 @@ class HipPopulationEngine(PopulationEngine):
             add_chunked("copy", 0, c_rows, H.COPY_DTYPE, c_cnt, 1)
             for o, n in fallbacks:
                 plan.launches.append(Launch("fn", 0, None, None, 0, self._fallback_fwd(mem, o, n, inputs, B, train)))
+
+        if imcol:
+            rows_ = [v["desc"] for v in imcol.values()]
+            cnt_ = [-(-v["rows"] // H.IMCOL_ROWS) for v in imcol.values()]
+            tiles_ = H.chunk_tiles(cnt_, 1)
+            plan.launches.insert(0, Launch("imcol", 0, desc_tensor(rows_, H.IMCOL_DTYPE), T(tiles_), len(tiles_)))
 
         # ---- loss ------------------------------------------------------------------------------
         if metrics is not None:
@@ -648,12 +690,18 @@ class HipPopulationEngine(PopulationEngine):
                             ab_cnt.append(H.red_chunks(M, F))
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-                        if fused:
-                            # v2: dZ = dY * act'(Y) on load, bias grad = extra ones-column of im2col
+                        ic = raw_conv_imcol(o, n) if fused and not head else None
+                        if ic is not None:
+                            wg_rows.append(dict(a=dz, b=ic["buf"].data_ptr(), out=gptr(lay.w[n.id]), bias=dbias,
+                                                aux=yv, act=act, H=OH, W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1,
+                                                SH=1, SW=1, M=F, N=K, K=M, flags=vec))
+                            wg_dims.append((F, K, M))
+                        elif fused:
+                            # v2: dZ = dY * act'(Y) on load; the bias gradient is reduced inside WGRAD
                             wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), bias=dbias, aux=yv, act=act,
                                                 H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW,
                                                 M=F, N=K, K=M, flags=vec))
-                            wg_dims.append((F, K + (1 if dbias else 0), M))
+                            wg_dims.append((F, K, M))
                         else:
                             wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
                                                 KH=KH, KW=KW, SH=SH, SW=SW, M=F, N=K, K=M, flags=vec))

@@ -59,7 +59,7 @@ def check_layouts():
     sizes = lib().desc_sizes()
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
-                     ("TransDesc", TRANS_DTYPE)]:
+                     ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
@@ -77,6 +77,8 @@ def ptr(t) -> int:
 # tile tables
 # ------------------------------------------------------------------------------------------------
 TRANS_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "F", "P", "C"]])
+IMCOL_DTYPE = np.dtype([(f, _I) for f in ["x", "out", "B", "H", "W", "OH", "OW", "KH", "KW", "SH", "SW", "K8"]])
+IMCOL_ROWS = 64
 TRANS_ELEMS = 4096
 
 
