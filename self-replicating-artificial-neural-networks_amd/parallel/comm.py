@@ -66,9 +66,13 @@ class TorchDistComm(Comm):
         self.torch = torch
         if not dist.is_initialized():
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
+                backend = os.environ.get("SERANN_COMM_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
+            if backend == "nccl":
+                # bind this rank to its GPU before RCCL creates communicators
+                lr = int(os.environ.get("LOCAL_RANK", "0"))
+                torch.cuda.set_device(lr % max(1, torch.cuda.device_count()))
             dist.init_process_group(backend=backend, timeout=timedelta(seconds=timeout_s))
         self.backend = dist.get_backend()
         self.rank = dist.get_rank()
