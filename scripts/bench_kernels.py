@@ -74,7 +74,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         cls = ""
-        if la.kind in ("gemm", "gemm2"):
+        if la.kind in ("gemm", "gemm2", "gemm3"):
             d = np.frombuffer(la.descs.cpu().numpy().tobytes(), dtype=H.GEMM_DTYPE)
             kinds = set()
             for r in d:
@@ -85,7 +85,7 @@ def main():
                 else:
                     kinds.add("dense")
             cls = "+".join(sorted(kinds))
-            mode = la.arg[0] if la.kind == "gemm2" else la.arg
+            mode = la.arg[0] if la.kind in ("gemm2", "gemm3") else la.arg
             flops = float(sum(2.0 * r["M"] * r["N"] * r["K"] for r in d))
         else:
             flops = 0.0

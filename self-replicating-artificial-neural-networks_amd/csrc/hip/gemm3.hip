@@ -1,0 +1,596 @@
+// Grouped implicit-GEMM convolution, v3 (CDNA4 MFMA) -- the engine's default path.
+//
+// Measured bottleneck of v2 (gemm2.hip): the im2col / col2im address math, not the MFMAs.  v2
+// decomposed every 8-element reduction chunk with two runtime integer divisions (k / C, pix / KW;
+// ~20 VALU instructions each -- CDNA has no integer divider) and 64-bit flat addresses, so a
+// 16-column tile issued ~10x more VALU cycles than MFMA cycles.  v3:
+//  * divisions by problem constants are host-computed magic multiplies (GemmDesc::dv*):
+//    q = (umulhi(n, mul) + n) >> shift;
+//  * operands are read with raw BUFFER loads: base address and extent in SGPRs (one resource per
+//    operand), 32-bit byte offsets per lane, and hardware range checking -- an out-of-range offset
+//    returns zeros, which is how invalid DGRAD taps, padded rows and tensor tails are zeroed without
+//    selects or branches;
+//  * the reduction chunk (kh, kw, c) is decomposed once per lane and k-step and shared by the RT
+//    row tiles of the wave (RT = 4: every weight fragment feeds 4 MFMAs), and the k loop is a
+//    two-register-set software pipeline (no fragment copies);
+//  * chunks are classified by contiguity: the 8 elements are contiguous in memory whenever they stay
+//    inside one receptive-field row (KW*C elements); only chunks that wrap to the next kernel row are
+//    spliced from a second 16-B load.  Problems with KW*C < 8 (FWD/WGRAD) or F % 8 != 0 on a
+//    KHxKW > 1 kernel (DGRAD) -- tiny and rare (mutants) -- use the GEN=true instantiation with
+//    element gathers, so the common kernel carries no gather code.
+//   FWD   : Y[m][f]  = act(im2col(X)[m][k] . Wm[f][k] + b[f])
+//   DGRAD : dX[m][c] = sum_{k'=(kh,kw,f)} dZ[b,(ih-kh)/SH,(iw-kw)/SW,f] . Wt[c][k']
+//   WGRAD : dWm[f][k] += sum_m dZ[m][f] . im2col(X)[m][k]      (LDS tiles, transposing LDS reads,
+//           64 rows of m per barrier pair, fp32 atomics into the gradient arena for split-m)
+// dZ = dY * act'(Y) is formed on the fly from the layer output Y (GemmDesc::aux) in DGRAD / WGRAD.
+#include "common.h"
+#include "serann_hip.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+namespace {
+
+union Frag {
+    uint4 u;
+    u32x4_t q;
+    uint32_t w[4];
+    bf16_t h[8];
+    bf16x8_t v;
+};
+
+// ---- buffer resources ------------------------------------------------------------------------
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int OOB = 0x7ffffff0;                 // byte offset beyond every extent: loads return 0
+
+// Range checking is per load instruction: a 16-B load that crosses num_records returns zeros as a
+// whole, so every extent carries 16 B of slack (the engine allocates >= 64 B of slack behind every
+// tensor it hands to these kernels; the over-read bytes are masked by splice()).
+__device__ __forceinline__ rsrc_t mkrsrc(int64_t ptr, int64_t bytes) {
+    bytes = bytes > 0 ? bytes + 16 : 0;
+    const int n = bytes > 0x7fff0000LL ? 0x7fff0000 : (int)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ uint4 bl16(rsrc_t r, int elem) {       // 8 bf16 at element offset (<0: zeros)
+    Frag f;
+    f.q = __builtin_amdgcn_raw_buffer_load_b128(r, elem < 0 ? OOB : elem * 2, 0, 0);
+    return f.u;
+}
+__device__ __forceinline__ bf16_t bl1(rsrc_t r, int elem) {
+    return __builtin_amdgcn_raw_buffer_load_b16(r, elem * 2, 0, 0);
+}
+
+// ---- fast division ---------------------------------------------------------------------------
+struct Div {
+    uint32_t mul, sh;
+};
+__device__ __forceinline__ Div mkdiv(int64_t packed) {
+    Div d;
+    d.mul = (uint32_t)(packed & 0xffffffffLL);
+    d.sh = (uint32_t)((packed >> 32) & 0xff);
+    return d;
+}
+__device__ __forceinline__ int fdiv(int n, const Div& d) {
+    return (int)((__umulhi((uint32_t)n, d.mul) + (uint32_t)n) >> d.sh);
+}
+
+struct G3 {
+    int H, W, C, OH, OW, F, KH, KW, SH, SW, M, N, K, act, flags;
+    Div dC, dKW, dOW, dOHW, dF, dW, dHW, dSH, dSW;
+};
+
+__device__ __forceinline__ G3 geo3(const GemmDesc& d) {
+    G3 g;
+    g.H = (int)d.H; g.W = (int)d.W; g.C = (int)d.C; g.OH = (int)d.OH; g.OW = (int)d.OW; g.F = (int)d.F;
+    g.KH = (int)d.KH; g.KW = (int)d.KW; g.SH = (int)d.SH; g.SW = (int)d.SW;
+    g.M = (int)d.M; g.N = (int)d.N; g.K = (int)d.K; g.act = (int)d.act; g.flags = (int)d.flags;
+    g.dC = mkdiv(d.dvC); g.dKW = mkdiv(d.dvKW); g.dOW = mkdiv(d.dvOW); g.dOHW = mkdiv(d.dvOHW);
+    g.dF = mkdiv(d.dvF); g.dW = mkdiv(d.dvW); g.dHW = mkdiv(d.dvHW); g.dSH = mkdiv(d.dvSH); g.dSW = mkdiv(d.dvSW);
+    return g;
+}
+
+// elements j < s from lo, j >= s from hi (s <= 0: all hi, s >= 8: all lo)
+__device__ __forceinline__ uint4 splice(uint4 lo, uint4 hi, int s) {
+    Frag a, b, r;
+    a.u = lo;
+    b.u = hi;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int e0 = 2 * w;
+        const uint32_t mixed = (a.w[w] & 0xffffu) | (b.w[w] & 0xffff0000u);
+        r.w[w] = (e0 + 1 < s) ? a.w[w] : ((e0 >= s) ? b.w[w] : mixed);
+    }
+    return r.u;
+}
+
+__device__ __forceinline__ uint4 mul_act_grad(uint4 dy, uint4 yv, int act) {
+    Frag g, y, out;
+    g.u = dy;
+    y.u = yv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out.h[j] = f2bf(bf2f(g.h[j]) * act_grad_from_y(bf2f(y.h[j]), act));
+    return out.u;
+}
+
+// ---- im2col chunk (FWD A operand, WGRAD B operand) -------------------------------------------
+// Per-lane decomposition of the reduction chunk starting at k = (kh, kw, c).
+struct KChunk {
+    int poff;     // element offset of (kh, kw, c) relative to the receptive field's top-left pixel
+    int run;      // elements usable from poff (>= 8: the whole chunk)
+    int noff;     // next kernel row's first element minus run (splice source); < 0: none (zeros)
+};
+
+__device__ __forceinline__ KChunk im2col_chunk(const G3& g, int k) {
+    KChunk r;
+    const int rem = g.K - k;
+    const int kk = min(k, g.K - 1);
+    const int pix = fdiv(kk, g.dC);
+    const int c = kk - pix * g.C;
+    const int kh = fdiv(pix, g.dKW);
+    const int kw = pix - kh * g.KW;
+    const int rowrun = (g.KW - kw) * g.C - c;            // elements left in this kernel row
+    const bool flat = g.W == g.KW || rowrun >= 8;         // kernel rows adjacent in memory, or no wrap
+    r.poff = (kh * g.W + kw) * g.C + c;
+    r.run = rem <= 0 ? 0 : (flat ? min(8, rem) : rowrun);
+    r.noff = (!flat && kh + 1 < g.KH) ? (kh + 1) * g.W * g.C - rowrun : -1;
+    return r;
+}
+
+// the chunk's 8 elements for the receptive field at `base` (GEN: KW*C < 8 problems gather)
+template <bool GEN>
+__device__ __forceinline__ uint4 im2col_load(rsrc_t x, const G3& g, int base, const KChunk& kc, int k) {
+    uint4 lo = bl16(x, base + kc.poff);
+    if (kc.run < 8) {                                      // K tail / kernel-row wrap (divergent, rare)
+        if (GEN && g.KW * g.C < 8) {
+            Frag f;
+            f.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int kk = k + j;
+                if (kk < g.K) {
+                    const int p = fdiv(kk, g.dC);
+                    const int c = kk - p * g.C;
+                    const int kh = fdiv(p, g.dKW);
+                    const int kw = p - kh * g.KW;
+                    f.h[j] = bl1(x, base + (kh * g.W + kw) * g.C + c);
+                }
+            }
+            lo = f.u;
+        } else {
+            const uint4 hi = kc.noff >= 0 ? bl16(x, base + kc.noff) : make_uint4(0, 0, 0, 0);
+            lo = splice(lo, hi, kc.run);
+        }
+    }
+    return lo;
+}
+
+}  // namespace
+
+// ==================================================================================================
+// FWD / DGRAD direct-fragment kernel.  NT = BN/16 column tiles, RT = 16-row tiles per wave.
+//   KW = false: block = 4 waves x RT*16 rows; every wave runs the whole k range.
+//   KW = true : block = RT*16 rows; the 4 waves split the k range (k-steps w, w+4, ...) and reduce
+//               their accumulators through LDS -- for few-row / long-K problems (merged Dense, heads).
+template <int MODE, int NT, int RT, bool KW, bool GEN>
+__global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restrict__ descs,
+                                                        const int4* __restrict__ tiles) {
+    constexpr int WROWS = RT * 16;
+    constexpr int BMB = KW ? WROWS : 4 * WROWS, BNB = NT * 16;
+    __shared__ float red[KW ? 3 * RT * NT * 4 * 64 : 1];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    const int m_w = td.y * BMB + (KW ? 0 : wave * WROWS);
+    const int n0 = td.z * BNB;
+    const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
+
+    // operand extents (elements): FWD A = X[B][H][W][C], DGRAD A = dZ (and Y) [B][OH][OW][F]
+    int64_t a_elems;
+    if (MODE == MODE_FWD) a_elems = (int64_t)(g.M / (g.OH * g.OW)) * g.H * g.W * g.C;
+    else a_elems = (int64_t)(g.M / (g.H * g.W)) * g.OH * g.OW * g.F;
+    const rsrc_t rA = mkrsrc(d.a, a_elems * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? a_elems * 2 : 0);
+    const rsrc_t rB = mkrsrc(d.b, (int64_t)g.N * g.K * 2);
+
+    // per-lane row invariants.  Rows >= M only feed accumulator rows that are never stored.
+    int base[RT], rb[RT], rih[RT], riw[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        int m = m_w + i * 16 + r16;
+        if (m >= g.M) m = 0;
+        if (MODE == MODE_FWD) {
+            const int b = fdiv(m, g.dOHW);
+            const int r = m - b * (g.OH * g.OW);
+            const int oh = fdiv(r, g.dOW);
+            const int ow = r - oh * g.OW;
+            base[i] = ((b * g.H + oh * g.SH) * g.W + ow * g.SW) * g.C;
+            rb[i] = rih[i] = riw[i] = 0;
+        } else {
+            const int b = fdiv(m, g.dHW);
+            const int r = m - b * (g.H * g.W);
+            rb[i] = b * g.OH;
+            rih[i] = fdiv(r, g.dW);
+            riw[i] = r - rih[i] * g.W;
+            base[i] = 0;
+        }
+    }
+    // B rows: columns n >= N only feed output columns that are never stored (clamped)
+    int brow[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) brow[j] = min(n0 + j * 16 + r16, g.N - 1) * g.K;
+
+    f32x4_t acc[RT][NT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto load = [&](Frag (&fa)[RT], Frag (&fb)[NT], int kt) {
+        const int k = kt * 32 + kg;
+        if (MODE == MODE_FWD) {
+            const KChunk kc = im2col_chunk(g, k);
+#pragma unroll
+            for (int i = 0; i < RT; ++i) fa[i].u = im2col_load<GEN>(rA, g, base[i], kc, k);
+        } else {
+            // k' = (kh*KW + kw)*F + f
+            const int rem = g.K - k;
+            const int kc = min(k, g.K - 1);
+            const int pix = fdiv(kc, g.dF);
+            const int f = kc - pix * g.F;
+            const int kh = fdiv(pix, g.dKW);
+            const int kw = pix - kh * g.KW;
+            const int run = rem <= 0 ? 0 : min(8, g.F - f);   // contiguous problems: F%8==0 or 1x1
+            if (!GEN || g.F - f >= 8 || g.KH * g.KW == 1) {
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const int ohn = rih[i] - kh, own = riw[i] - kw;
+                    int oh = ohn, ow = own;
+                    bool ok = ohn >= 0 && own >= 0;
+                    if (g.SH != 1) { oh = fdiv(max(ohn, 0), g.dSH); ok = ok && oh * g.SH == ohn; }
+                    if (g.SW != 1) { ow = fdiv(max(own, 0), g.dSW); ok = ok && ow * g.SW == own; }
+                    ok = ok && oh < g.OH && ow < g.OW;
+                    const int off = ok ? ((rb[i] + oh) * g.OW + ow) * g.F + f : -1;
+                    uint4 v = bl16(rA, off);
+                    if (g.act != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), g.act);
+                    fa[i].u = v;
+                }
+                if (run < 8) {
+#pragma unroll
+                    for (int i = 0; i < RT; ++i) fa[i].u = splice(fa[i].u, make_uint4(0, 0, 0, 0), run);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    Frag t;
+                    t.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int kk = k + j;
+                        if (kk >= g.K) continue;
+                        const int p = fdiv(kk, g.dF);
+                        const int ff = kk - p * g.F;
+                        const int kh2 = fdiv(p, g.dKW);
+                        const int kw2 = p - kh2 * g.KW;
+                        const int ohn = rih[i] - kh2, own = riw[i] - kw2;
+                        int oh = ohn, ow = own;
+                        bool ok = ohn >= 0 && own >= 0;
+                        if (g.SH != 1) { oh = fdiv(max(ohn, 0), g.dSH); ok = ok && oh * g.SH == ohn; }
+                        if (g.SW != 1) { ow = fdiv(max(own, 0), g.dSW); ok = ok && ow * g.SW == own; }
+                        ok = ok && oh < g.OH && ow < g.OW;
+                        if (!ok) continue;
+                        const int off = ((rb[i] + oh) * g.OW + ow) * g.F + ff;
+                        float v = bf2f(bl1(rA, off));
+                        if (g.act != ACT_LINEAR) v *= act_grad_from_y(bf2f(bl1(rY, off)), g.act);
+                        t.h[j] = f2bf(v);
+                    }
+                    fa[i] = t;
+                }
+            }
+        }
+        const int kb = min(k, g.K);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) fb[j].u = bl16(rB, brow[j] + kb);
+        if (k + 8 > g.K) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) fb[j].u = splice(fb[j].u, make_uint4(0, 0, 0, 0), g.K - k);
+        }
+    };
+    auto mma = [&](const Frag (&fa)[RT], const Frag (&fb)[NT]) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
+    };
+
+    // two-register-set software pipeline: fragments of step s+1 load while step s multiplies.  The
+    // loop body is branch-free so the accumulators stay in place (no AGPR shuffles at the latch).
+    const int kstep = KW ? 4 : 1;
+    const int kfirst = kt0 + (KW ? wave : 0);
+    const int nsteps = kfirst < kt1 ? (kt1 - kfirst + kstep - 1) / kstep : 0;
+    Frag fa0[RT], fb0[NT], fa1[RT], fb1[NT];
+    if (nsteps > 0) load(fa0, fb0, kfirst);
+    int st = 0;
+    for (; st + 2 < nsteps; st += 2) {
+        load(fa1, fb1, kfirst + (st + 1) * kstep);
+        mma(fa0, fb0);
+        load(fa0, fb0, kfirst + (st + 2) * kstep);
+        mma(fa1, fb1);
+    }
+    if (st + 1 < nsteps) {
+        load(fa1, fb1, kfirst + (st + 1) * kstep);
+        mma(fa0, fb0);
+        mma(fa1, fb1);
+    } else if (st < nsteps) {
+        mma(fa0, fb0);
+    }
+
+    if (KW) {
+        if (wave > 0) {
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        red[((((wave - 1) * RT + i) * NT + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (wave > 0) return;
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][j][r] += red[(((w * RT + i) * NT + j) * 4 + r) * 64 + lane];
+    }
+
+    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    const int rq = (lane >> 4) * 4;
+    const float* bias = reinterpret_cast<const float*>(d.bias);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = n0 + j * 16 + r16;
+        if (col >= g.N) continue;
+        const float bv = (MODE == MODE_FWD && bias) ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m_w + i * 16 + rq + r;
+                if (row >= g.M) continue;
+                float v = acc[i][j][r];
+                const int64_t off = (int64_t)row * g.N + col;
+                if (MODE == MODE_FWD) {
+                    v = apply_act(v + bv, g.act);
+                    if (g.flags & GF_OUT_F32) {
+                        reinterpret_cast<float*>(d.out)[off] = v;
+                        continue;
+                    }
+                }
+                bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
+                if (g.flags & GF_ACCUM) v += bf2f(o[off]);
+                o[off] = f2bf(v);
+            }
+    }
+}
+
+// ==================================================================================================
+// WGRAD: dWm[f][k] += sum_m dZ[m][f] * im2col(X)[m][k].  Tile BMF (f) x BNK (k), 64 rows of m per
+// step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
+// in LDS in that layout with 16-B writes; MFMA fragments come from ds_read_b64_tr_b16.
+template <int BMF, int BNK, bool GEN>
+__global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                       const int4* __restrict__ tiles) {
+    constexpr int BKM = 64;
+    constexpr int LDA = BMF + 8, LDB = BNK + 8;
+    __shared__ __attribute__((aligned(16))) bf16_t As[BKM * LDA];
+    __shared__ __attribute__((aligned(16))) bf16_t Bs[BKM * LDB];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
+    const int f0 = td.y * BMF, k0c = td.z * BNK;
+    const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // in units of 32 rows of m
+    const int mlim = min(g.K, kt1 * 32);
+    float* __restrict__ dbias = reinterpret_cast<float*>(d.bias);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int ohw = g.OH * g.OW;
+    const int64_t nb = g.K / ohw;                              // batch
+    const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
+    const rsrc_t rX = mkrsrc(d.b, nb * g.H * g.W * g.C * 2);
+
+    constexpr int WR = (BMF == 64) ? 2 : 1;          // waves along f
+    constexpr int WC = 4 / WR;                       // waves along k
+    constexpr int TF = BMF / WR / 16;
+    constexpr int TK = BNK / WC / 16;
+    const int wf = wave / WC, wk = wave % WC;
+
+    // A loader: rows m (64) x f (BMF) in chunks of 8 f
+    constexpr int ACH = BMF / 8;
+    constexpr int AROWS = 256 / ACH;                 // rows per pass
+    constexpr int APASS = (BKM + AROWS - 1) / AROWS;
+    const int a_f = (t % ACH) * 8, a_r = t / ACH;
+    const bool a_act = a_r < BKM;
+    const int a_nv = min(8, g.F - (f0 + a_f));       // valid f of this chunk (may be <= 0)
+    // B loader: rows m (64) x k (BNK) in chunks of 8 k; the k chunk is fixed per thread
+    constexpr int BCH = BNK / 8;
+    constexpr int BROWS = 256 / BCH;
+    constexpr int BPASS = BKM / BROWS;
+    const int b_k = (t % BCH) * 8, b_r = t / BCH;
+    const int kk = k0c + b_k;
+    G3 gx = g;                                       // im2col width is N (= KH*KW*C)
+    gx.K = g.N;
+    const KChunk kc = im2col_chunk(gx, kk);
+
+    Frag ra[APASS], rbv[BPASS];
+    auto load = [&](int kt) {
+        const int m0 = kt * 32;
+#pragma unroll
+        for (int p = 0; p < APASS; ++p) {
+            const int r = a_r + p * AROWS;
+            const int m = m0 + r;
+            const bool ok = a_act && r < BKM && a_nv > 0 && m < mlim;
+            const int off = ok ? m * g.F + f0 + a_f : -1;
+            uint4 v = bl16(rZ, off);
+            if (g.act != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), g.act);
+            if (a_nv < 8) v = splice(v, make_uint4(0, 0, 0, 0), a_nv);
+            ra[p].u = v;
+        }
+#pragma unroll
+        for (int p = 0; p < BPASS; ++p) {
+            const int m = m0 + b_r + p * BROWS;
+            if (m < mlim) {
+                const int b = fdiv(m, g.dOHW);
+                const int r = m - b * ohw;
+                const int oh = fdiv(r, g.dOW);
+                const int ow = r - oh * g.OW;
+                const int base = ((b * g.H + oh * g.SH) * g.W + ow * g.SW) * g.C;
+                rbv[p].u = im2col_load<GEN>(rX, gx, base, kc, kk);
+            } else {
+                rbv[p].u = make_uint4(0, 0, 0, 0);
+            }
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int p = 0; p < APASS; ++p) {
+            const int r = a_r + p * AROWS;
+            if (a_act && r < BKM) *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = ra[p].u;
+        }
+#pragma unroll
+        for (int p = 0; p < BPASS; ++p)
+            *reinterpret_cast<uint4*>(&Bs[(b_r + p * BROWS) * LDB + b_k]) = rbv[p].u;
+    };
+
+    f32x4_t acc[TF][TK];
+#pragma unroll
+    for (int i = 0; i < TF; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const bool do_bias = dbias != nullptr && td.z == 0;
+    float bsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+
+    // kt counts 32-row units; one iteration consumes two of them (64 rows)
+    if (kt0 < kt1) load(kt0);
+    for (int kt = kt0; kt < kt1; kt += 2) {
+        __syncthreads();
+        stash();
+        if (do_bias) {
+#pragma unroll
+            for (int p = 0; p < APASS; ++p)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[j] += bf2f(ra[p].h[j]);
+        }
+        __syncthreads();
+        if (kt + 2 < kt1) load(kt + 2);
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int mr = sub * 32 + grp * 8 + q;
+            Frag fa[TF], fbk[TK];
+#pragma unroll
+            for (int i = 0; i < TF; ++i) {
+                const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
+                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&As[mr * LDA + col]));
+                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&As[(mr + 4) * LDA + col]));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { fa[i].h[e] = (bf16_t)lo[e]; fa[i].h[4 + e] = (bf16_t)hi[e]; }
+            }
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = wk * (BNK / WC) + j * 16 + 4 * pp;
+                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[mr * LDB + col]));
+                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(mr + 4) * LDB + col]));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { fbk[j].h[e] = (bf16_t)lo[e]; fbk[j].h[4 + e] = (bf16_t)hi[e]; }
+            }
+#pragma unroll
+            for (int i = 0; i < TF; ++i)
+#pragma unroll
+                for (int j = 0; j < TK; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fbk[j].v, acc[i][j], 0, 0, 0);
+        }
+    }
+
+    if (do_bias) {
+        // lanes of one wave holding the same f chunk differ in the bits >= log2(ACH)
+#pragma unroll
+        for (int xo = ACH; xo < 64; xo <<= 1)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
+        if (a_act && lane < ACH) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+        }
+    }
+    const int c16 = lane & 15, rq = (lane >> 4) * 4;
+    float* out = reinterpret_cast<float*>(d.out);
+#pragma unroll
+    for (int i = 0; i < TF; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j) {
+            const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
+            if (col >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
+                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+            }
+        }
+}
+
+// variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN
+// variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
+void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipStream_t s = as_stream(stream);
+    const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
+    const int4* tp = as_ptr<const int4>(tiles);
+    dim3 grid((unsigned)ntiles), block(256);
+    if (mode == MODE_WGRAD) {
+        const bool gen = variant >= 1000000;
+        const int v = variant % 1000000;
+#define W3(BMF_, BNK_) \
+    if (v == BMF_ * 1000 + BNK_) { \
+        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return; }
+        W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64)
+#undef W3
+        throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
+    }
+    const bool gen = variant >= 1000;
+    const bool kw = (variant % 1000) >= 100;
+    const int rt = (variant / 10) % 10;
+    const int nt = variant % 10;
+#define D3(MODE_, NT_, RT_, KW_) \
+    if (mode == MODE_ && nt == NT_ && rt == RT_ && kw == KW_) { \
+        if (gen) hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, KW_, true>), grid, block, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, KW_, false>), grid, block, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return; }
+#define D3ALL(MODE_) \
+    D3(MODE_, 1, 4, false) D3(MODE_, 2, 4, false) D3(MODE_, 4, 4, false) \
+    D3(MODE_, 1, 2, false) D3(MODE_, 2, 2, false) D3(MODE_, 4, 2, false) D3(MODE_, 8, 2, false) \
+    D3(MODE_, 1, 2, true) D3(MODE_, 2, 2, true) D3(MODE_, 4, 2, true) D3(MODE_, 8, 2, true)
+    D3ALL(MODE_FWD)
+    D3ALL(MODE_DGRAD)
+#undef D3ALL
+#undef D3
+    throw std::runtime_error("gemm3: unknown variant " + std::to_string(variant));
+}

@@ -27,6 +27,8 @@ PYBIND11_MODULE(serann_hip, m) {
           py::arg("ntiles"), py::arg("stream"));
     m.def("gemm2", &launch_gemm2, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
           py::arg("ntiles"), py::arg("stream"));
+    m.def("gemm3", &launch_gemm3, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
+          py::arg("ntiles"), py::arg("stream"));
     m.def("transpose_weights", &launch_transpose_weights);
     m.def("adam", &launch_adam);
     m.def("f32_to_bf16", &launch_f32_to_bf16);

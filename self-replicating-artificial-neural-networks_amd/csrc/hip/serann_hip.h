@@ -10,6 +10,9 @@ struct GemmDesc {
     int64_t H, W, C, OH, OW, F, KH, KW, SH, SW;
     int64_t M, N, K;
     int64_t act, flags;
+    // host-computed fast-division magics (low 32 bits: multiplier, bits 32..39: shift) of the
+    // divisors the v3 kernels need: q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31.
+    int64_t dvC, dvKW, dvOW, dvOHW, dvF, dvW, dvHW, dvSH, dvSW;
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
@@ -21,6 +24,7 @@ enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
 void launch_grouped_gemm(int mode, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_gemm2(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 
 // ---- optimizer --------------------------------------------------------------------------------

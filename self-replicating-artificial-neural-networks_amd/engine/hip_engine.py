@@ -36,7 +36,16 @@ from .base import FitResult, PopulationEngine, TrainConfig, epoch_permutation
 import os
 
 ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp32
-GEMM_IMPL = os.environ.get("SERANN_GEMM", "v2")   # v2: direct-fragment FWD/DGRAD + tr-read WGRAD; v1: LDS tiles
+SLACK = 64  # elements of zeroed tail on every arena
+# v3 (default): buffer-load direct-fragment FWD/DGRAD with magic-number im2col + 64-row WGRAD;
+# v2: first direct-fragment version; v1: LDS-tiled version.  Kept selectable for A/B measurements.
+GEMM_IMPL = os.environ.get("SERANN_GEMM", "v3")
+
+
+def _padded_zeros(shape, dtype, device) -> torch.Tensor:
+    """Zeroed tensor followed by SLACK zeroed elements (GEMM fragment loads may over-read)."""
+    n = math.prod(shape)
+    return torch.zeros(n + SLACK, dtype=dtype, device=device)[:n].view(shape)
 
 
 def _al(n: int) -> int:
@@ -57,7 +66,9 @@ class Arena:
         return off
 
     def materialize(self, zero=True):
-        self.t = (torch.zeros if zero else torch.empty)(max(self.size, ALIGN), dtype=self.dtype, device=self.device)
+        # +SLACK: the GEMM kernels' 16-B fragment loads may run a few elements past a tensor's end
+        self.t = (torch.zeros if zero else torch.empty)(max(self.size, ALIGN) + SLACK, dtype=self.dtype,
+                                                        device=self.device)
         return self.t
 
     def view(self, off: int, n: int) -> torch.Tensor:
@@ -127,6 +138,8 @@ class Plan:
             k = la.kind
             if k == "gemm":
                 L.grouped_gemm(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "gemm3":
+                L.gemm3(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "gemm2":
                 L.gemm2(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "transpose":
@@ -208,12 +221,12 @@ class HipPopulationEngine(PopulationEngine):
                 d[nid] = wt_size
                 wt_size += _al(cnt)
             self.wt_off.append(d)
-        self.wt = torch.zeros(max(wt_size, ALIGN), dtype=torch.bfloat16, device=dev)
+        self.wt = torch.zeros(max(wt_size, ALIGN) + SLACK, dtype=torch.bfloat16, device=dev)
         self.p = self.parena.materialize()
         self.g = torch.zeros_like(self.p)
         self.m = torch.zeros_like(self.p)
         self.v = torch.zeros_like(self.p)
-        self.pbf = torch.zeros(self.p.numel(), dtype=torch.bfloat16, device=dev)
+        self.pbf = torch.zeros(self.p.numel() + SLACK, dtype=torch.bfloat16, device=dev)
         self.stats = self.sarena.materialize()
         self.step_i = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr_t = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -266,7 +279,7 @@ class HipPopulationEngine(PopulationEngine):
                             P.narrow(0, lay.beta[n.id], c).zero_()
                         self.stats.narrow(0, lay.mm[n.id], c).zero_()
                         self.stats.narrow(0, lay.mv[n.id], c).fill_(1.0)
-            self.pbf.copy_(P.to(torch.bfloat16))
+            self.pbf[:P.numel()].copy_(P.to(torch.bfloat16))
 
     def export_params(self, i: int) -> Dict[int, Dict[str, np.ndarray]]:
         """Organism ``i`` parameters in Keras layout (for parity tests / checkpoints)."""
@@ -424,6 +437,8 @@ class HipPopulationEngine(PopulationEngine):
             for i, r in enumerate(rows):
                 for k, v in r.items():
                     a[i][k] = v
+            if dtype == H.GEMM_DTYPE:
+                H.fill_gemm_divisors(a)
             return T(np.frombuffer(a.tobytes(), dtype=np.uint8).copy())
 
         def add_gemm(mode_, rows, dims):
@@ -437,19 +452,20 @@ class HipPopulationEngine(PopulationEngine):
                 if len(tiles):
                     plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
                 return
+            v3 = GEMM_IMPL == "v3"
             groups = {}
             for r, dm in zip(rows, dims):
-                v = H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
+                v = H.gemm3_variant(mode_, dm[0], dm[1], dm[2], r) if v3 else H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
                 groups.setdefault(v, ([], []))
                 groups[v][0].append({k: val for k, val in r.items() if k != "b_v1"})
                 groups[v][1].append(dm)
             for v in sorted(groups):
                 rws, dms = groups[v]
-                bm, bn = H.gemm2_block(mode_, v)
+                bm, bn = H.gemm3_block(mode_, v) if v3 else H.gemm2_block(mode_, v)
                 tiles = H.gemm_tiles(dms, mode_, bm=bm, bn=bn)
                 if len(tiles):
-                    plan.launches.append(Launch("gemm2", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
-                                                len(tiles)))
+                    plan.launches.append(Launch("gemm3" if v3 else "gemm2", (mode_, v),
+                                                desc_tensor(rws, H.GEMM_DTYPE), T(tiles), len(tiles)))
 
         def add_chunked(kind, arg, rows, dtype, counts, chunk):
             if not rows:
@@ -961,8 +977,8 @@ class HipPopulationEngine(PopulationEngine):
         xcols, gcols = dd["train_x"].shape[1], dd["train_g"].shape[1]
 
         # shared batch buffers
-        xb = torch.zeros(B, xcols, dtype=torch.bfloat16, device=dev)
-        gb = torch.zeros(B, gcols, dtype=torch.bfloat16, device=dev)
+        xb = _padded_zeros((B, xcols), torch.bfloat16, dev)
+        gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
         yb = torch.zeros(B, dtype=torch.int32, device=dev)
         self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
         perm_t = torch.zeros(max(split, 1), dtype=torch.int32, device=dev)
@@ -1102,8 +1118,8 @@ class HipPopulationEngine(PopulationEngine):
             dev = self.device
             xcols = self.layouts[0].ir.nodes[0].shape[0] * self.layouts[0].ir.nodes[0].shape[1]
             gcols = self.layouts[0].ir.genotype_size
-            xb = torch.zeros(B, xcols, dtype=torch.bfloat16, device=dev)
-            gb = torch.zeros(B, gcols, dtype=torch.bfloat16, device=dev)
+            xb = _padded_zeros((B, xcols), torch.bfloat16, dev)
+            gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
             yb = torch.zeros(B, dtype=torch.int32, device=dev)
             metrics = torch.zeros(self.num_organisms, 4, dtype=torch.float32, device=dev)
             self._input_tensors = getattr(self, "_input_tensors", {})
@@ -1153,8 +1169,8 @@ class HipPopulationEngine(PopulationEngine):
         dev = self.device
         for c0 in range(0, pool, B):
             nb = min(B, pool - c0)
-            xs = torch.zeros(P, B, images[0][0].size, dtype=torch.bfloat16, device=dev)
-            gs = torch.zeros(P, B, self.layouts[0].ir.genotype_size, dtype=torch.bfloat16, device=dev)
+            xs = _padded_zeros((P, B, images[0][0].size), torch.bfloat16, dev)
+            gs = _padded_zeros((P, B, self.layouts[0].ir.genotype_size), torch.bfloat16, dev)
             xs[:, :nb] = torch.as_tensor(np.stack([im[c0:c0 + nb].reshape(nb, -1) for im in images]),
                                          dtype=torch.float32, device=dev).to(torch.bfloat16)
             gs[:, :nb] = torch.as_tensor(np.asarray(genotypes, np.float32), device=dev)[:, None, :].to(torch.bfloat16)

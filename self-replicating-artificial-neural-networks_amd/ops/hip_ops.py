@@ -12,7 +12,9 @@ from ..utils.native import load
 
 _I = np.int64
 GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "KH", "KW", "SH", "SW",
-               "M", "N", "K", "act", "flags"]
+               "M", "N", "K", "act", "flags",
+               # fast-division magics for the v3 kernels (filled by fill_gemm_divisors)
+               "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW"]
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 ACTBWD_DTYPE = np.dtype([(f, _I) for f in ["dy", "y", "dz", "dbias", "M", "N", "act", "flags"]])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
@@ -32,6 +34,39 @@ BM, BN, BK = 64, 64, 32
 RED_ELEMS = 16384      # aux.hip: elements per block of the channel-strided reductions (BN, act_bwd)
 POOL_ELEMS = 1024
 COPY_ROWS = 16
+
+
+def fast_div_magic(d: int) -> int:
+    """Packed (multiplier | shift << 32) for q = (umulhi(n, mul) + n) >> shift == n // d, exact for
+    0 <= n < 2**31 (gemm3.hip fdiv)."""
+    d = max(int(d), 1)
+    sh = (d - 1).bit_length()
+    mul = ((1 << 32) * ((1 << sh) - d)) // d + 1
+    return int(mul | (sh << 32))
+
+
+def fill_gemm_divisors(a: np.ndarray) -> np.ndarray:
+    """Fill the dv* fields of a GEMM_DTYPE record array from its geometry fields (in place)."""
+    for r in a:
+        r["dvC"] = fast_div_magic(r["C"])
+        r["dvKW"] = fast_div_magic(r["KW"])
+        r["dvOW"] = fast_div_magic(r["OW"])
+        r["dvOHW"] = fast_div_magic(r["OH"] * r["OW"])
+        r["dvF"] = fast_div_magic(r["F"])
+        r["dvW"] = fast_div_magic(r["W"])
+        r["dvHW"] = fast_div_magic(r["H"] * r["W"])
+        r["dvSH"] = fast_div_magic(r["SH"])
+        r["dvSW"] = fast_div_magic(r["SW"])
+    return a
+
+
+def gemm_desc_array(rows) -> np.ndarray:
+    """dict rows -> GEMM_DTYPE records with the fast-division fields filled."""
+    a = np.zeros(len(rows), dtype=GEMM_DTYPE)
+    for i, r in enumerate(rows):
+        for k, v in r.items():
+            a[i][k] = v
+    return fill_gemm_divisors(a)
 
 
 def red_chunks(rows: int, channels: int) -> int:
@@ -90,6 +125,37 @@ def gemm2_variant(mode: int, M: int, N: int, K: int = 0) -> int:
     if mode != MODE_WGRAD and M <= 8192 and -(-K // BK) >= 16:
         v += 1000
     return v
+
+
+def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
+    """Kernel instantiation of the v3 kernels (gemm3.hip launch_gemm3 encoding) for one problem.
+
+    FWD/DGRAD: NT (BN/16) + 10*RT + 100*KW + 1000*GEN; WGRAD: BMF*1000 + BNK + 1000000*GEN.
+    GEN (element-gather fallback) only for problems whose reduction chunks can wrap more than one
+    kernel row (KW*C < 8) or straddle output pixels in DGRAD (F % 8 != 0 on a KHxKW > 1 kernel)."""
+    KH, KW, C, W, F = (int(geo.get(k, 1)) for k in ("KH", "KW", "C", "W", "F"))
+    im2col_gen = KW * C < 8 and W != KW and KH > 1
+    if mode == MODE_WGRAD:
+        bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
+        if bmf == 16:
+            bnk = 256 if N > 128 else (128 if N > 64 else 64)
+        else:
+            bnk = 128 if N > 64 else 64
+        return bmf * 1000 + bnk + (1000000 if im2col_gen else 0)
+    gen = im2col_gen if mode == MODE_FWD else (F % 8 != 0 and KH * KW > 1)
+    nt = 1 if N <= 16 else (2 if N <= 32 else (4 if N <= 64 else 8))
+    kw = M <= 8192 and -(-K // BK) >= 16
+    rt = 2 if (kw or nt == 8 or M < 16384) else 4
+    return nt + 10 * rt + (100 if kw else 0) + (1000 if gen else 0)
+
+
+def gemm3_block(mode: int, variant: int):
+    """(rows, cols) of the output tile one block of a v3 launch covers."""
+    if mode == MODE_WGRAD:
+        v = variant % 1000000
+        return (v // 1000, v % 1000)
+    nt, rt, kw = variant % 10, (variant // 10) % 10, (variant % 1000) >= 100
+    return (16 * rt if kw else 64 * rt, 16 * nt)
 
 
 def gemm2_block(mode: int, variant: int):

@@ -25,6 +25,8 @@ def _desc(rows, dtype):
     for i, r in enumerate(rows):
         for k, v in r.items():
             a[i][k] = v
+    if dtype == H.GEMM_DTYPE:
+        H.fill_gemm_divisors(a)
     return torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=DEV)
 
 
@@ -33,6 +35,15 @@ def _run_gemm(mode, rows, dims, impl="v1"):
         d = _desc(rows, H.GEMM_DTYPE)
         t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
         H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    elif impl == "v3":
+        groups = {}
+        for r, dm in zip(rows, dims):
+            groups.setdefault(H.gemm3_variant(mode, dm[0], dm[1], dm[2], r), []).append((r, dm))
+        for v, items in groups.items():
+            d = _desc([r for r, _ in items], H.GEMM_DTYPE)
+            bm, bn = H.gemm3_block(mode, v)
+            t = torch.as_tensor(H.gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn), device=DEV)
+            H.lib().gemm3(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
     else:
         groups = {}
         for r, dm in zip(rows, dims):
@@ -54,10 +65,18 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     (7, 1, 1, 868, 110, 1, 1, 1, 1, "linear"),
     (2, 26, 26, 8, 8, 1, 3, 1, 2, "relu"),
     (3, 10, 10, 24, 9, 7, 7, 1, 1, "linear"),
+    # v3 paths: RT=4 rows/wave (M >= 16384), odd C with kernel-row wraps, NT=8 (N > 64), stride 3,
+    # KW*C < 8 gathers (GEN), F % 8 != 0 conv DGRAD (GEN)
+    (48, 24, 24, 20, 32, 5, 5, 1, 1, "relu"),
+    (6, 28, 28, 55, 64, 7, 7, 1, 1, "linear"),
+    (4, 6, 6, 40, 100, 3, 3, 1, 1, "relu"),
+    (3, 20, 20, 16, 16, 3, 3, 3, 3, "linear"),
+    (2, 11, 11, 2, 13, 3, 3, 2, 2, "linear"),
+    (30, 30, 1, 3, 24, 7, 1, 1, 1, "relu"),
 ]
 
 
-@pytest.mark.parametrize("impl", ["v1", "v2"])
+@pytest.mark.parametrize("impl", ["v1", "v2", "v3"])
 @pytest.mark.parametrize("shape", SHAPES)
 def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     B, Hh, Ww, C, Fo, KH, KW, SH, SW, act = shape
@@ -107,7 +126,7 @@ def test_transpose_weights_kernel():
     assert torch.equal(out, w.permute(3, 1, 2, 0).contiguous())
 
 
-@pytest.mark.parametrize("impl", ["v1", "v2"])
+@pytest.mark.parametrize("impl", ["v1", "v2", "v3"])
 def test_grouped_gemm_many_problems_one_launch(impl):
     rows, dims, refs, outs = [], [], [], []
     keep = []
@@ -223,9 +242,10 @@ def test_loss_kernel_matches_keras_losses():
     assert abs(metrics[2].item() / B - mse.item()) < 1e-5
 
 
+@pytest.mark.parametrize("impl", ["v2", "v3"])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
-def test_v2_fused_act_grad_and_bias_grad(act):
-    """v2 WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient."""
+def test_fused_act_grad_and_bias_grad(act, impl):
+    """v2/v3 WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient."""
     B, Hh, Ww, C, Fo, KH, KW, SH, SW = 3, 9, 9, 8, 13, 3, 3, 1, 1
     OH, OW = Hh - 2, Ww - 2
     x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
@@ -242,7 +262,7 @@ def test_v2_fused_act_grad_and_bias_grad(act):
     db = torch.zeros(Fo, device=DEV)
     _run_gemm(H.MODE_WGRAD, [dict(a=dy.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), bias=db.data_ptr(),
                                   aux=y.data_ptr(), act=H.ACT_CODES[act], M=Fo, N=K, K=B * OH * OW, **geo)],
-              [(Fo, K, B * OH * OW)], "v2")
+              [(Fo, K, B * OH * OW)], impl)
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)
     ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
@@ -252,20 +272,25 @@ def test_v2_fused_act_grad_and_bias_grad(act):
     wt = w.permute(3, 1, 2, 0).contiguous()
     _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), aux=y.data_ptr(),
                                   act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
-              [(B * Hh * Ww, C, KH * KW * Fo)], "v2")
+              [(B * Hh * Ww, C, KH * KW * Fo)], impl)
     ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref_dx) < 6e-3
 
 
-def test_v2_wave_split_k_dense():
+@pytest.mark.parametrize("impl", ["v2", "v3"])
+def test_wave_split_k_dense(impl):
     """Few rows, long K (the Dense-on-merge shape): the wave-split-K form must match."""
     M, K, N = 750, 5003, 110
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / 70).bfloat16()
     b = torch.randn(N, device=DEV)
     y = torch.zeros(M, N, device=DEV)
-    assert H.gemm2_variant(H.MODE_FWD, M, N, K) >= 1000
-    _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=1, W=1, C=K,
-                                OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=K, flags=H.GF_OUT_F32)],
-              [(M, N, K)], "v2")
+    geo = dict(H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1)
+    if impl == "v2":
+        assert H.gemm2_variant(H.MODE_FWD, M, N, K) >= 1000
+    else:
+        assert 100 <= H.gemm3_variant(H.MODE_FWD, M, N, K, geo) % 1000
+    _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), M=M, N=N, K=K,
+                                flags=H.GF_OUT_F32, **geo)],
+              [(M, N, K)], impl)
     assert _rel(y, x.float() @ w.float().t() + b) < 1e-4
