@@ -166,6 +166,55 @@ __device__ __forceinline__ uint4 im2col_load(rsrc_t x, const G3& g, int base, co
     return lo;
 }
 
+// ---- coalesced epilogue ------------------------------------------------------------------------
+// A wave's accumulator tile covers rows [row0, row0 + nrows) x ALL N columns of a row-major [M][N]
+// bf16 output, i.e. one contiguous range of memory.  The MFMA C layout gives each lane 4 rows of one
+// column (2-byte scattered stores), so the tile is first written to LDS in the output's own layout
+// (row stride N) and then streamed out with 16-B stores (read-modify-write for GF_ACCUM).  row0 * N
+// is a multiple of 16 elements for every caller (row0 is a multiple of 32), so the 16-B chunks are
+// aligned.
+template <int RT, int NT>
+__device__ __forceinline__ void wave_store_rows(bf16_t* __restrict__ st, bf16_t* __restrict__ out, int64_t row0,
+                                                int nrows, int N, bool accum, const f32x4_t (&acc)[RT][NT],
+                                                const float* __restrict__ bias, int act, int lane) {
+    const int r16 = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = j * 16 + r16;
+        if (col >= N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = i * 16 + rq + r;
+                st[row * N + col] = f2bf(apply_act(acc[i][j][r] + bv, act));
+            }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = nrows * N;
+    const int nvec = total >> 3;
+    bf16_t* __restrict__ dst = out + row0 * N;
+    for (int v = lane; v < nvec; v += 64) {
+        Frag f;
+        f.u = *reinterpret_cast<const uint4*>(&st[v * 8]);
+        if (accum) {
+            Frag o;
+            o.u = *reinterpret_cast<const uint4*>(&dst[v * 8]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(o.h[e]));
+        }
+        *reinterpret_cast<uint4*>(&dst[v * 8]) = f.u;
+    }
+    for (int e = nvec * 8 + lane; e < total; e += 64) {
+        float v = bf2f(st[e]);
+        if (accum) v += bf2f(dst[e]);
+        dst[e] = f2bf(v);
+    }
+}
+
 }  // namespace
 
 // ==================================================================================================
@@ -173,12 +222,17 @@ __device__ __forceinline__ uint4 im2col_load(rsrc_t x, const G3& g, int base, co
 //   KW = false: block = 4 waves x RT*16 rows; every wave runs the whole k range.
 //   KW = true : block = RT*16 rows; the 4 waves split the k range (k-steps w, w+4, ...) and reduce
 //               their accumulators through LDS -- for few-row / long-K problems (merged Dense, heads).
-template <int MODE, int NT, int RT, bool KW, bool GEN>
+template <int MODE, int NT, int RT, bool KW, bool GEN, bool SK = false>
 __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restrict__ descs,
                                                         const int4* __restrict__ tiles) {
     constexpr int WROWS = RT * 16;
     constexpr int BMB = KW ? WROWS : 4 * WROWS, BNB = NT * 16;
-    __shared__ float red[KW ? 3 * RT * NT * 4 * 64 : 1];
+    // KW: cross-wave reduction buffer (re-used by wave 0 as the output staging tile);
+    // otherwise one output staging tile per wave
+    constexpr int RED = KW ? 3 * RT * NT * 4 * 64 : 1;
+    constexpr int STAGE = KW ? 1 : 4 * WROWS * BNB;
+    __shared__ __attribute__((aligned(16))) float red[RED];
+    __shared__ __attribute__((aligned(16))) bf16_t ostage[STAGE];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);
@@ -307,26 +361,36 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
     };
 
-    // two-register-set software pipeline: fragments of step s+1 load while step s multiplies.  The
-    // loop body is branch-free so the accumulators stay in place (no AGPR shuffles at the latch).
-    const int kstep = KW ? 4 : 1;
-    const int kfirst = kt0 + (KW ? wave : 0);
-    const int nsteps = kfirst < kt1 ? (kt1 - kfirst + kstep - 1) / kstep : 0;
-    Frag fa0[RT], fb0[NT], fa1[RT], fb1[NT];
-    if (nsteps > 0) load(fa0, fb0, kfirst);
-    int st = 0;
-    for (; st + 2 < nsteps; st += 2) {
-        load(fa1, fb1, kfirst + (st + 1) * kstep);
-        mma(fa0, fb0);
-        load(fa0, fb0, kfirst + (st + 2) * kstep);
-        mma(fa1, fb1);
-    }
-    if (st + 1 < nsteps) {
-        load(fa1, fb1, kfirst + (st + 1) * kstep);
-        mma(fa0, fb0);
-        mma(fa1, fb1);
-    } else if (st < nsteps) {
-        mma(fa0, fb0);
+    if (SK) {
+        // K <= 32: one k step, one fragment set (fewer registers -> more resident waves for the
+        // store-bound small-K layers)
+        Frag fa0[RT], fb0[NT];
+        if (kt0 < kt1) {
+            load(fa0, fb0, kt0);
+            mma(fa0, fb0);
+        }
+    } else {
+        // two-register-set software pipeline: fragments of step s+1 load while step s multiplies.  The
+        // loop body is branch-free so the accumulators stay in place (no AGPR shuffles at the latch).
+        const int kstep = KW ? 4 : 1;
+        const int kfirst = kt0 + (KW ? wave : 0);
+        const int nsteps = kfirst < kt1 ? (kt1 - kfirst + kstep - 1) / kstep : 0;
+        Frag fa0[RT], fb0[NT], fa1[RT], fb1[NT];
+        if (nsteps > 0) load(fa0, fb0, kfirst);
+        int st = 0;
+        for (; st + 2 < nsteps; st += 2) {
+            load(fa1, fb1, kfirst + (st + 1) * kstep);
+            mma(fa0, fb0);
+            load(fa0, fb0, kfirst + (st + 2) * kstep);
+            mma(fa1, fb1);
+        }
+        if (st + 1 < nsteps) {
+            load(fa1, fb1, kfirst + (st + 1) * kstep);
+            mma(fa0, fb0);
+            mma(fa1, fb1);
+        } else if (st < nsteps) {
+            mma(fa0, fb0);
+        }
     }
 
     if (KW) {
@@ -352,9 +416,20 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
                         acc[i][j][r] += red[(((w * RT + i) * NT + j) * 4 + r) * 64 + lane];
     }
 
-    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
-    const int rq = (lane >> 4) * 4;
+    // epilogue: one contiguous output range per wave when the block spans all N columns
     const float* bias = reinterpret_cast<const float*>(d.bias);
+    if (n0 == 0 && g.N <= BNB && !(g.flags & GF_OUT_F32)) {
+        const int nrows = min(WROWS, g.M - m_w);
+        if (nrows > 0) {
+            bf16_t* st = KW ? reinterpret_cast<bf16_t*>(red) : &ostage[wave * WROWS * BNB];
+            wave_store_rows<RT, NT>(st, reinterpret_cast<bf16_t*>(d.out), m_w, nrows, g.N,
+                                    (g.flags & GF_ACCUM) != 0, acc, MODE == MODE_FWD ? bias : nullptr,
+                                    MODE == MODE_FWD ? g.act : ACT_LINEAR, lane);
+        }
+        return;
+    }
+    // C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    const int rq = (lane >> 4) * 4;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int col = n0 + j * 16 + r16;
@@ -407,7 +482,8 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
     const rsrc_t rX = mkrsrc(d.b, nb * g.H * g.W * g.C * 2);
 
-    constexpr int WR = (BMF == 64) ? 2 : 1;          // waves along f
+    // BNK = 16 (layers with <= 16 reduction columns, e.g. Dense on the raw image): the 4 waves split f
+    constexpr int WR = (BNK == 16) ? 4 : ((BMF == 64) ? 2 : 1);   // waves along f
     constexpr int WC = 4 / WR;                       // waves along k
     constexpr int TF = BMF / WR / 16;
     constexpr int TK = BNK / WC / 16;
@@ -423,7 +499,7 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     // B loader: rows m (64) x k (BNK) in chunks of 8 k; the k chunk is fixed per thread
     constexpr int BCH = BNK / 8;
     constexpr int BROWS = 256 / BCH;
-    constexpr int BPASS = BKM / BROWS;
+    constexpr int BPASS = (BKM + BROWS - 1) / BROWS;
     const int b_k = (t % BCH) * 8, b_r = t / BCH;
     const int kk = k0c + b_k;
     G3 gx = g;                                       // im2col width is N (= KH*KW*C)
@@ -447,7 +523,7 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
 #pragma unroll
         for (int p = 0; p < BPASS; ++p) {
             const int m = m0 + b_r + p * BROWS;
-            if (m < mlim) {
+            if (m < mlim && b_r + p * BROWS < BKM) {
                 const int b = fdiv(m, g.dOHW);
                 const int r = m - b * ohw;
                 const int oh = fdiv(r, g.dOW);
@@ -467,7 +543,7 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
         }
 #pragma unroll
         for (int p = 0; p < BPASS; ++p)
-            *reinterpret_cast<uint4*>(&Bs[(b_r + p * BROWS) * LDB + b_k]) = rbv[p].u;
+            if (b_r + p * BROWS < BKM) *reinterpret_cast<uint4*>(&Bs[(b_r + p * BROWS) * LDB + b_k]) = rbv[p].u;
     };
 
     f32x4_t acc[TF][TK];
@@ -555,14 +631,401 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
         }
 }
 
-// variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN
+// ==================================================================================================
+// FWD convolution with the input patch staged in LDS ("halo" tile).  A block covers TM = 64*RT
+// consecutive output pixels of ONE image (x BN = 16*NT filters): the input rows they touch are one
+// contiguous range of the NHWC tensor, copied once into LDS with the channel count padded to
+// Cp = ceil8(C) (pad channels zero) and an odd number of 16-B slots per pixel (bank spread).  Every
+// A fragment (output pixel x 8 channels of one tap) is then one aligned ds_read_b128 -- the kh*kw-fold
+// re-reads of im2col are served by LDS instead of the vector-memory pipeline, and odd channel counts
+// no longer produce misaligned global loads.  The reduction runs over (tap, padded channel) in
+// 32-element MFMA k-steps; the matching weight tile [BN][32] is staged in LDS once per block and
+// step (double-buffered, one barrier per step) and shared by the 4 waves.
+// PATCH = LDS patch capacity in bf16 elements: 8192 / 16384 / 32768 (16 / 32 / 64 KB; with the weight
+// tiles that allows about 8 / 4 / 2 resident blocks per CU).
+template <int NT, int RT, int PATCH>
+__global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __restrict__ descs,
+                                                          const int4* __restrict__ tiles) {
+    constexpr int TM = 64 * RT, BN = NT * 16, LDBS = 40;
+    // the patch region doubles as the output staging tile after the k loop
+    __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH > TM * BN ? PATCH : TM * BN];
+    __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN * LDBS];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);
+    const Div dCp = mkdiv(d.dvCp);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    const int ohw = g.OH * g.OW;
+    const int b = td.y, m0 = td.z, n0 = td.w * BN;
+    const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
+    const int Cs = (C8 & 1) ? Cp : Cp + 8;             // LDS pixel stride (odd count of 16-B slots)
+    const int oh_a = fdiv(m0, g.dOW);
+    const int m_last = min(m0 + TM, ohw) - 1;
+    const int oh_b = fdiv(m_last, g.dOW);
+    const int rows_in = (oh_b - oh_a) * g.SH + g.KH;
+    const int npix = rows_in * g.W;
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+
+    // ---- stage the patch: input rows [oh_a*SH, oh_a*SH + rows_in) of image b ----------------------
+    const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * g.H * g.W * g.C * 2);
+    const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
+    for (int p = t; p < npix; p += 256) {
+        for (int c = 0; c < Cp; c += 8) {
+            uint4 v = bl16(rA, gbase + p * g.C + c);
+            if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+            *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
+        }
+    }
+
+    // ---- per-lane row offsets into the patch ----------------------------------------------------
+    int rowoff[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        int m = m0 + (wave * RT + i) * 16 + r16;
+        if (m > m_last) m = m0;
+        const int oh = fdiv(m, g.dOW);
+        const int ow = m - oh * g.OW;
+        rowoff[i] = ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+    }
+
+    // ---- weight tile loader: thread -> (column bn, 8-element chunk bkg) --------------------------
+    const int taps = g.KH * g.KW;
+    const int nsteps = (taps * Cp + 31) / 32;
+    const rsrc_t rB = mkrsrc(d.b, (int64_t)g.N * g.K * 2);
+    const int bn = t >> 2, bkg = (t & 3) * 8;
+    const int brow = min(n0 + bn, g.N - 1) * g.K;
+    auto gload_b = [&](int s) -> uint4 {
+        const int e = s * 32 + bkg;
+        const int tap = fdiv(e, dCp);
+        const int c = e - tap * Cp;
+        if (bn >= BN || tap >= taps || c >= g.C) return zero;
+        uint4 v = bl16(rB, brow + tap * g.C + c);
+        if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+        return v;
+    };
+
+    f32x4_t acc[RT][NT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    uint4 breg = gload_b(0);
+    if (bn < BN) *reinterpret_cast<uint4*>(&Bs[0][bn * LDBS + bkg]) = breg;
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const int cur = s & 1;
+        if (s + 1 < nsteps) breg = gload_b(s + 1);
+        const int e = s * 32 + kg;
+        int tap = fdiv(e, dCp);
+        const int c = e - tap * Cp;
+        tap = min(tap, taps - 1);                       // past the end: finite A, zero B
+        const int kh = fdiv(tap, g.dKW);
+        const int kw = tap - kh * g.KW;
+        const int tapoff = (kh * g.W + kw) * Cs + c;
+        Frag fa[RT], fb[NT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) fa[i].u = *reinterpret_cast<const uint4*>(&patch[rowoff[i] + tapoff]);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+            fb[j].u = *reinterpret_cast<const uint4*>(&Bs[cur][(j * 16 + r16) * LDBS + kg]);
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
+        if (s + 1 < nsteps && bn < BN) *reinterpret_cast<uint4*>(&Bs[cur ^ 1][bn * LDBS + bkg]) = breg;
+        __syncthreads();
+    }
+
+    // ---- epilogue ---------------------------------------------------------------------------------
+    const float* bias = reinterpret_cast<const float*>(d.bias);
+    bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
+    const int64_t rowbase = (int64_t)b * ohw;
+    if (n0 == 0 && g.N <= BN && !(g.flags & GF_OUT_F32)) {
+        // the block's rows are consecutive pixels of one image: contiguous output rows
+        const int mw = m0 + wave * RT * 16;
+        const int nrows = min(RT * 16, m_last + 1 - mw);
+        if (nrows > 0)
+            wave_store_rows<RT, NT>(&patch[wave * RT * 16 * BN], o, rowbase + mw, nrows, g.N,
+                                    (g.flags & GF_ACCUM) != 0, acc, bias, g.act, lane);
+        return;
+    }
+    const int rq = (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = n0 + j * 16 + r16;
+        if (col >= g.N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + (wave * RT + i) * 16 + rq + r;
+                if (m > m_last) continue;
+                const int64_t off = (rowbase + m) * g.N + col;
+                float v = apply_act(acc[i][j][r] + bv, g.act);
+                if (g.flags & GF_OUT_F32) {
+                    reinterpret_cast<float*>(d.out)[off] = v;
+                    continue;
+                }
+                if (g.flags & GF_ACCUM) v += bf2f(o[off]);
+                o[off] = f2bf(v);
+            }
+    }
+}
+
+// ==================================================================================================
+// WGRAD of a KHxKW > 1 convolution with the input patch staged in LDS.
+//   dWm[f][tap][c] += sum_m dZ[m][f] * X[patch(m) + tap][c]
+// A block owns an f tile (BMF) x a k' tile (BNK columns of the padded (tap, Cp) reduction space) and
+// sweeps a range of 128-pixel chunks [td.z, td.w) (chunk = (image, pixel tile)).  Per chunk it stages
+// the chunk's input rows (padded channels, as in g3_conv_fwd_kernel) and its 128 dZ rows (act' applied)
+// in LDS; both MFMA operands are then read with ds_read_b64_tr_b16 -- the B operand (im2col) with
+// per-lane addresses into the patch, so every input element is fetched from global once per chunk
+// instead of KH*KW times.  Accumulators stay in registers across chunks; one fp32 atomic flush at the
+// end (the bias gradient is reduced by the k'-tile-0 blocks from the staged dZ rows).
+template <int BMF, int BNK, int PATCH>
+__global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                            const int4* __restrict__ tiles) {
+    constexpr int TM = 128, LDA = BMF + 8;
+    // patch + one 16-B dump slot for the staging writes of pieces past the chunk's patch
+    __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH + 8];
+    __shared__ __attribute__((aligned(16))) bf16_t As[TM * LDA];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
+    const Div dCp = mkdiv(d.dvCp);
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int f0 = (td.y >> 16) * BMF, kc0 = (td.y & 0xffff) * BNK;
+    const int ohw = g.OH * g.OW;
+    const int tpi = (ohw + TM - 1) / TM;
+    const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
+    const int Cs = (C8 & 1) ? Cp : Cp + 8;
+    const int taps = g.KH * g.KW;
+    const int nbatch = g.K / ohw;
+    const rsrc_t rX = mkrsrc(d.b, (int64_t)nbatch * g.H * g.W * g.C * 2);
+    const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
+    float* __restrict__ dbias = reinterpret_cast<float*>(d.bias);
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+
+    constexpr int WR = (BMF == 64) ? 2 : 1;          // waves along f
+    constexpr int WC = 4 / WR;                       // waves along k'
+    constexpr int TF = BMF / WR / 16;
+    constexpr int TK = BNK / WC / 16;
+    const int wf = wave / WC, wk = wave % WC;
+    const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+    // per-lane im2col column offsets: column k' = kc0 + wk*(BNK/WC) + j*16 + 4*pp (4 consecutive
+    // channels of one tap).  Columns past the reduction read a valid patch address (zero B is not
+    // needed: their accumulators are never stored).
+    int coff[TK];
+#pragma unroll
+    for (int j = 0; j < TK; ++j) {
+        const int kp = kc0 + wk * (BNK / WC) + j * 16 + 4 * pp;
+        int tap = fdiv(kp, dCp);
+        const int c = kp - tap * Cp;
+        tap = min(tap, taps - 1);
+        const int kh = fdiv(tap, g.dKW);
+        const int kw = tap - kh * g.KW;
+        coff[j] = (kh * g.W + kw) * Cs + c;
+    }
+
+    // dZ loader: rows m (TM) x f (BMF) in chunks of 8 f
+    constexpr int ACH = BMF / 8;
+    const int a_f = (t % ACH) * 8, a_r0 = t / ACH;
+    constexpr int AROWS = 256 / ACH;
+    const int a_nv = min(8, g.F - (f0 + a_f));
+    const bool do_bias = dbias != nullptr && kc0 == 0;
+    float bsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+
+    f32x4_t acc[TF][TK];
+#pragma unroll
+    for (int i = 0; i < TF; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // Software pipeline over chunks: the global loads of chunk ch+1 (patch and dZ rows) are issued
+    // into registers before the MFMAs of chunk ch and land in LDS after them, so their latency hides
+    // behind compute (one LDS copy of each operand; two barriers per chunk).
+    constexpr int PLD = PATCH / 2048;               // 16-B patch pieces per thread (max)
+    constexpr int ALD = (TM * ACH + 255) / 256;     // 16-B dZ pieces per thread
+    uint4 pre[PLD], apre[ALD];
+    int cur_npix = 0;
+    auto fetch = [&](int ch) {
+        const int b = ch / tpi;
+        const int m0 = (ch - b * tpi) * TM;
+        const int oh_a = fdiv(m0, g.dOW);
+        const int m_last = min(m0 + TM, ohw) - 1;
+        const int oh_b = fdiv(m_last, g.dOW);
+        const int npix = ((oh_b - oh_a) * g.SH + g.KH) * g.W;
+        const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
+        cur_npix = npix;
+#pragma unroll
+        for (int k = 0; k < PLD; ++k) {
+            const int u = t + k * 256;
+            const int p = fdiv(u * 8, dCp);
+            const int c = u * 8 - p * Cp;
+            pre[k] = bl16(rX, p < npix ? gbase + p * g.C + c : -1);
+        }
+        if (g.C & 7) {                                 // zero the pad channels (not in the K range)
+#pragma unroll
+            for (int k = 0; k < PLD; ++k) {
+                const int u = t + k * 256;
+                const int p = fdiv(u * 8, dCp);
+                const int c = u * 8 - p * Cp;
+                pre[k] = splice(pre[k], zero, g.C - c);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < ALD; ++k) {
+            const int r = a_r0 + k * AROWS;
+            const int m = m0 + r;
+            const bool ok = r < TM && a_nv > 0 && m <= m_last;
+            const int off = ok ? (b * ohw + m) * g.F + f0 + a_f : -1;
+            uint4 v = bl16(rZ, off);
+            if (g.act != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), g.act);
+            if (a_nv < 8) v = splice(v, zero, a_nv);
+            apre[k] = v;
+        }
+    };
+
+    if (td.z < td.w) fetch(td.z);
+    for (int ch = td.z; ch < td.w; ++ch) {
+        const int b = ch / tpi;
+        const int m0 = (ch - b * tpi) * TM;
+        const int oh_a = fdiv(m0, g.dOW);
+        const int m_last = min(m0 + TM, ohw) - 1;
+        const int npix = cur_npix;
+        __syncthreads();                              // previous chunk's LDS reads are done
+#pragma unroll
+        for (int k = 0; k < PLD; ++k) {
+            const int u = t + k * 256;
+            const int p = fdiv(u * 8, dCp);
+            const int c = u * 8 - p * Cp;
+            *reinterpret_cast<uint4*>(&patch[p < npix ? p * Cs + c : PATCH]) = pre[k];
+        }
+#pragma unroll
+        for (int k = 0; k < ALD; ++k) {
+            const int r = a_r0 + k * AROWS;
+            if (r < TM) {
+                *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = apre[k];
+                if (do_bias) {
+                    Frag fv;
+                    fv.u = apre[k];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bsum[j] += bf2f(fv.h[j]);
+                }
+            }
+        }
+        __syncthreads();
+        if (ch + 1 < td.w) fetch(ch + 1);
+#pragma unroll
+        for (int sub = 0; sub < TM / 32; ++sub) {
+            // rows of this lane's two tr-read quads; rows past the chunk end read a valid pixel
+            // (their dZ rows are zero)
+            int roff[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int m = m0 + sub * 32 + grp * 8 + 4 * h + q;
+                if (m > m_last) m = m0;
+                const int oh = fdiv(m, g.dOW);
+                const int ow = m - oh * g.OW;
+                roff[h] = ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+            }
+            const int mr = sub * 32 + grp * 8 + q;
+            Frag fa[TF], fbk[TK];
+#pragma unroll
+            for (int i = 0; i < TF; ++i) {
+                const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
+                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&As[mr * LDA + col]));
+                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&As[(mr + 4) * LDA + col]));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { fa[i].h[e] = (bf16_t)lo[e]; fa[i].h[4 + e] = (bf16_t)hi[e]; }
+            }
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&patch[roff[0] + coff[j]]));
+                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&patch[roff[1] + coff[j]]));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { fbk[j].h[e] = (bf16_t)lo[e]; fbk[j].h[4 + e] = (bf16_t)hi[e]; }
+            }
+#pragma unroll
+            for (int i = 0; i < TF; ++i)
+#pragma unroll
+                for (int j = 0; j < TK; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fbk[j].v, acc[i][j], 0, 0, 0);
+        }
+    }
+
+    if (do_bias) {
+#pragma unroll
+        for (int xo = ACH; xo < 64; xo <<= 1)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
+        if (lane < ACH && a_r0 < TM) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+        }
+    }
+    // flush: column k' -> (tap, c) -> dWm[f][tap*C + c] for c < C
+    const int c16 = lane & 15, rq = (lane >> 4) * 4;
+    float* out = reinterpret_cast<float*>(d.out);
+#pragma unroll
+    for (int j = 0; j < TK; ++j) {
+        const int kp = kc0 + wk * (BNK / WC) + j * 16 + c16;
+        const int tap = fdiv(kp, dCp);
+        const int c = kp - tap * Cp;
+        if (tap >= taps || c >= g.C) continue;
+        const int col = tap * g.C + c;
+#pragma unroll
+        for (int i = 0; i < TF; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
+                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+            }
+    }
+}
+
+// variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
+//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form
+//                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
+//                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
+//                 tiles (prob, b, m0, ntile)
 // variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
+//                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
+//                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
     hipStream_t s = as_stream(stream);
     const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
     const int4* tp = as_ptr<const int4>(tiles);
     dim3 grid((unsigned)ntiles), block(256);
+    if (mode == MODE_WGRAD && variant >= 3000000) {
+        const int tier = (variant / 100000) % 10;
+        const int v = variant % 100000;
+#define CW3T(BMF_, BNK_, TIER_, PATCH_)                                                               \
+    if (v == BMF_ * 1000 + BNK_ && tier == TIER_) {                                                   \
+        hipLaunchKernelGGL((g3_conv_wgrad_kernel<BMF_, BNK_, PATCH_>), grid, block, 0, s, dp, tp);     \
+        SERANN_CHECK(hipGetLastError());                                                              \
+        return;                                                                                       \
+    }
+#define CW3(BMF_, BNK_) CW3T(BMF_, BNK_, 0, 8192) CW3T(BMF_, BNK_, 1, 16384) CW3T(BMF_, BNK_, 2, 32768)
+        CW3(16, 512) CW3(16, 256) CW3(16, 128) CW3(32, 512) CW3(32, 256) CW3(32, 128) CW3(64, 256) CW3(64, 128)
+#undef CW3T
+#undef CW3
+        throw std::runtime_error("gemm3: unknown conv WGRAD variant " + std::to_string(variant));
+    }
     if (mode == MODE_WGRAD) {
         const bool gen = variant >= 1000000;
         const int v = variant % 1000000;
@@ -571,9 +1034,36 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
-        W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64)
+        W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
+    }
+    if (mode == MODE_FWD && variant >= 2000 && variant < 3000) {
+        const int v = variant - 2000;
+#define C3T(NT_, RT_, TIER_, PATCH_)                                                                  \
+    if (v == 100 * TIER_ + NT_ + 10 * RT_) {                                                          \
+        hipLaunchKernelGGL((g3_conv_fwd_kernel<NT_, RT_, PATCH_>), grid, block, 0, s, dp, tp);         \
+        SERANN_CHECK(hipGetLastError());                                                              \
+        return;                                                                                       \
+    }
+#define C3(NT_, RT_) C3T(NT_, RT_, 0, 8192) C3T(NT_, RT_, 1, 16384) C3T(NT_, RT_, 2, 32768)
+        C3(1, 1) C3(2, 1) C3(4, 1) C3(1, 2) C3(2, 2) C3(4, 2) C3(1, 4) C3(2, 4) C3(4, 4)
+#undef C3T
+#undef C3
+        throw std::runtime_error("gemm3: unknown conv variant " + std::to_string(variant));
+    }
+    if (variant >= 5000) {
+        const int v = variant - 5000;
+#define S3(MODE_, NT_, RT_)                                                                             \
+    if (mode == MODE_ && v == NT_ + 10 * RT_) {                                                         \
+        hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, false, false, true>), grid, block, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError());                                                                \
+        return;                                                                                         \
+    }
+        S3(MODE_FWD, 1, 4) S3(MODE_FWD, 2, 4) S3(MODE_FWD, 4, 4) S3(MODE_FWD, 8, 2)
+        S3(MODE_DGRAD, 1, 4) S3(MODE_DGRAD, 2, 4) S3(MODE_DGRAD, 4, 4) S3(MODE_DGRAD, 8, 2)
+#undef S3
+        throw std::runtime_error("gemm3: unknown single-step variant " + std::to_string(variant));
     }
     const bool gen = variant >= 1000;
     const bool kw = (variant % 1000) >= 100;

@@ -13,6 +13,7 @@ struct GemmDesc {
     // host-computed fast-division magics (low 32 bits: multiplier, bits 32..39: shift) of the
     // divisors the v3 kernels need: q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31.
     int64_t dvC, dvKW, dvOW, dvOHW, dvF, dvW, dvHW, dvSH, dvSW;
+    int64_t dvCp;     // magic of Cp = C rounded up to 8 (LDS-halo conv kernels)
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors

@@ -452,20 +452,26 @@ class HipPopulationEngine(PopulationEngine):
                 if len(tiles):
                     plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
                 return
-            v3 = GEMM_IMPL == "v3"
+            if GEMM_IMPL == "v3":
+                clean = [{k: val for k, val in r.items() if k != "b_v1"} for r in rows]
+                for v, rws, tiles in H.gemm3_plan(mode_, clean, dims):
+                    if len(tiles):
+                        plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
+                                                    len(tiles)))
+                return
             groups = {}
             for r, dm in zip(rows, dims):
-                v = H.gemm3_variant(mode_, dm[0], dm[1], dm[2], r) if v3 else H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
+                v = H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
                 groups.setdefault(v, ([], []))
                 groups[v][0].append({k: val for k, val in r.items() if k != "b_v1"})
                 groups[v][1].append(dm)
             for v in sorted(groups):
                 rws, dms = groups[v]
-                bm, bn = H.gemm3_block(mode_, v) if v3 else H.gemm2_block(mode_, v)
+                bm, bn = H.gemm2_block(mode_, v)
                 tiles = H.gemm_tiles(dms, mode_, bm=bm, bn=bn)
                 if len(tiles):
-                    plan.launches.append(Launch("gemm3" if v3 else "gemm2", (mode_, v),
-                                                desc_tensor(rws, H.GEMM_DTYPE), T(tiles), len(tiles)))
+                    plan.launches.append(Launch("gemm2", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
+                                                len(tiles)))
 
         def add_chunked(kind, arg, rows, dtype, counts, chunk):
             if not rows:

@@ -14,7 +14,7 @@ _I = np.int64
 GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "KH", "KW", "SH", "SW",
                "M", "N", "K", "act", "flags",
                # fast-division magics for the v3 kernels (filled by fill_gemm_divisors)
-               "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW"]
+               "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW", "dvCp"]
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 ACTBWD_DTYPE = np.dtype([(f, _I) for f in ["dy", "y", "dz", "dbias", "M", "N", "act", "flags"]])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
@@ -57,6 +57,7 @@ def fill_gemm_divisors(a: np.ndarray) -> np.ndarray:
         r["dvHW"] = fast_div_magic(r["H"] * r["W"])
         r["dvSH"] = fast_div_magic(r["SH"])
         r["dvSW"] = fast_div_magic(r["SW"])
+        r["dvCp"] = fast_div_magic(-(-int(r["C"]) // 8) * 8)
     return a
 
 
@@ -137,6 +138,8 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     im2col_gen = KW * C < 8 and W != KW and KH > 1
     if mode == MODE_WGRAD:
         bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
+        if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
+            return 64 * 1000 + 16 + (1000000 if im2col_gen else 0)
         if bmf == 16:
             bnk = 256 if N > 128 else (128 if N > 64 else 64)
         else:
@@ -144,6 +147,8 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
         return bmf * 1000 + bnk + (1000000 if im2col_gen else 0)
     gen = im2col_gen if mode == MODE_FWD else (F % 8 != 0 and KH * KW > 1)
     nt = 1 if N <= 16 else (2 if N <= 32 else (4 if N <= 64 else 8))
+    if K <= 32 and not gen and M >= 16384:       # single k step: store-bound, keep registers low
+        return 5000 + nt + 10 * (2 if nt == 8 else 4)
     kw = M <= 8192 and -(-K // BK) >= 16
     rt = 2 if (kw or nt == 8 or M < 16384) else 4
     return nt + 10 * rt + (100 if kw else 0) + (1000 if gen else 0)
@@ -154,8 +159,120 @@ def gemm3_block(mode: int, variant: int):
     if mode == MODE_WGRAD:
         v = variant % 1000000
         return (v // 1000, v % 1000)
+    if variant >= 5000:
+        return (64 * ((variant // 10) % 10), 16 * (variant % 10))
     nt, rt, kw = variant % 10, (variant // 10) % 10, (variant % 1000) >= 100
     return (16 * rt if kw else 64 * rt, 16 * nt)
+
+
+CONV_PATCH_TIERS = (8192, 16384, 32768)   # gemm3.hip: LDS patch capacities (bf16 elements)
+
+
+def conv_lds_config(geo: dict, N: int):
+    """(RT, patch tier) for the LDS-halo FWD conv kernel (64*RT output pixels per block), or None
+    when the problem is not a KHxKW > 1 convolution or its input patch does not fit in 64 KB.
+    Prefers the largest RT (more MFMA work per staged patch and per barrier) whose padding of the
+    per-image pixel count stays within 20% of the smallest tiling, then the smallest patch tier that
+    holds it (more blocks resident per CU)."""
+    KH, KW, C, W, OH, OW, SH = (int(geo[k]) for k in ("KH", "KW", "C", "W", "OH", "OW", "SH"))
+    if KH * KW <= 1:
+        return None
+    cp = -(-C // 8) * 8
+    cs = cp if (cp // 8) % 2 == 1 else cp + 8
+    ohw = OH * OW
+    min_pad = -(-ohw // 64) * 64
+    for rt in (4, 2, 1):
+        tm = 64 * rt
+        if -(-ohw // tm) * tm > 1.2 * min_pad and rt > 1:
+            continue
+        span = (OW - 1 + tm - 1) // OW
+        need = (span * SH + KH) * W * cs
+        for tier, cap in enumerate(CONV_PATCH_TIERS):
+            if need <= cap:
+                return rt, tier
+    return None
+
+
+def conv_wgrad_config(geo: dict, F: int):
+    """(BMF, BNK, patch tier) for the LDS-halo conv WGRAD kernel (128-pixel chunks), or None."""
+    KH, KW, C, W, OH, OW, SH = (int(geo[k]) for k in ("KH", "KW", "C", "W", "OH", "OW", "SH"))
+    if KH * KW <= 1:
+        return None
+    cp = -(-C // 8) * 8
+    cs = cp if (cp // 8) % 2 == 1 else cp + 8
+    span = (OW - 1 + 127) // OW
+    need = (span * SH + KH) * W * cs
+    tier = next((i for i, cap in enumerate(CONV_PATCH_TIERS) if need <= cap), None)
+    if tier is None:
+        return None
+    kp = KH * KW * cp
+    bmf = 16 if F <= 16 else (32 if F <= 32 else 64)
+    if bmf == 64:
+        bnk = 256 if kp > 128 else 128
+    else:
+        bnk = 512 if kp >= 384 else (256 if kp > 128 else 128)
+    return bmf, bnk, tier
+
+
+def gemm3_plan(mode: int, rows, dims):
+    """Group the problems of one grouped launch by v3 kernel instantiation.
+
+    Returns [(variant, rows, tiles int32 (n, 4))].  FWD convolutions whose input patch fits in LDS go
+    to the halo kernel (tiles (prob, image, first pixel, column tile)); everything else to the
+    direct / WGRAD kernels (tiles (prob, m tile, n tile, k range))."""
+    groups = {}
+    for r, dm in zip(rows, dims):
+        M, N, K = dm
+        v = None
+        if mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
+            cfg = conv_lds_config(r, N)
+            if cfg is not None:
+                nt = 1 if N <= 16 else (2 if N <= 32 else 4)
+                v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
+        if mode == MODE_WGRAD:
+            cfg = conv_wgrad_config(r, M)
+            if cfg is not None:
+                v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
+        if v is None:
+            v = gemm3_variant(mode, M, N, K, r)
+        groups.setdefault(v, []).append((r, dm))
+    out = []
+    for v in sorted(groups):
+        items = groups[v]
+        if 2000 <= v < 3000 and mode == MODE_FWD:
+            nt, rt = v % 10, (v // 10) % 10
+            tm, bn = 64 * rt, 16 * nt
+            tl = []
+            for p, (r, (M, N, K)) in enumerate(items):
+                ohw = int(r["OH"]) * int(r["OW"])
+                nb = M // ohw
+                tpi = -(-ohw // tm)
+                ntn = -(-N // bn)
+                bb, jj, nn = np.meshgrid(np.arange(nb), np.arange(tpi), np.arange(ntn), indexing="ij")
+                tl.append(np.stack([np.full(bb.size, p), bb.ravel(), jj.ravel() * tm, nn.ravel()], 1))
+            tiles = np.concatenate(tl).astype(np.int32)
+        elif v >= 3000000 and mode == MODE_WGRAD:
+            bmf, bnk = (v % 100000) // 1000, v % 1000
+            tl = []
+            for p, (r, (M, N, K)) in enumerate(items):
+                ohw = int(r["OH"]) * int(r["OW"])
+                nchunks = (K // ohw) * (-(-ohw // 128))
+                cp = -(-int(r["C"]) // 8) * 8
+                nkt = -(-(int(r["KH"]) * int(r["KW"]) * cp) // bnk)
+                nft = -(-M // bmf)
+                per = min(64, max(8, -(-nchunks // 64)))
+                for c0 in range(0, nchunks, per):
+                    c1 = min(nchunks, c0 + per)
+                    ff, kk = np.meshgrid(np.arange(nft), np.arange(nkt), indexing="ij")
+                    n = ff.size
+                    tl.append(np.stack([np.full(n, p), (ff.ravel() << 16) | kk.ravel(), np.full(n, c0),
+                                        np.full(n, c1)], 1))
+            tiles = np.concatenate(tl).astype(np.int32)
+        else:
+            bm, bn = gemm3_block(mode, v)
+            tiles = gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn)
+        out.append((v, [r for r, _ in items], tiles))
+    return out
 
 
 def gemm2_block(mode: int, variant: int):

@@ -36,13 +36,9 @@ def _run_gemm(mode, rows, dims, impl="v1"):
         t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
         H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
     elif impl == "v3":
-        groups = {}
-        for r, dm in zip(rows, dims):
-            groups.setdefault(H.gemm3_variant(mode, dm[0], dm[1], dm[2], r), []).append((r, dm))
-        for v, items in groups.items():
-            d = _desc([r for r, _ in items], H.GEMM_DTYPE)
-            bm, bn = H.gemm3_block(mode, v)
-            t = torch.as_tensor(H.gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn), device=DEV)
+        for v, rws, tiles in H.gemm3_plan(mode, rows, dims):
+            d = _desc(rws, H.GEMM_DTYPE)
+            t = torch.as_tensor(tiles, device=DEV)
             H.lib().gemm3(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
     else:
         groups = {}
@@ -73,6 +69,9 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     (3, 20, 20, 16, 16, 3, 3, 3, 3, "linear"),
     (2, 11, 11, 2, 13, 3, 3, 2, 2, "linear"),
     (30, 30, 1, 3, 24, 7, 1, 1, 1, "relu"),
+    # single-k-step FWD/DGRAD (K <= 32, M >= 16384) and the narrow (N <= 16) WGRAD layout
+    (30, 28, 28, 1, 100, 1, 1, 1, 1, "relu"),
+    (25, 26, 26, 24, 40, 1, 1, 1, 1, "sigmoid"),
 ]
 
 
@@ -294,3 +293,30 @@ def test_wave_split_k_dense(impl):
                                 flags=H.GF_OUT_F32, **geo)],
               [(M, N, K)], impl)
     assert _rel(y, x.float() @ w.float().t() + b) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(4, 12, 12, 16, 32, 3, 3, 1, 1), (3, 1, 1, 200, 37, 1, 1, 1, 1),
+                                   (40, 10, 10, 24, 64, 1, 1, 1, 1)])
+def test_v3_accumulating_outputs(shape):
+    """GF_ACCUM (a tensor with several consumers): DGRAD and FWD add into the existing bf16 output,
+    through both the coalesced LDS-staged epilogue and the scattered one."""
+    B, Hh, Ww, C, Fo, KH, KW, SH, SW = shape
+    OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
+    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
+    w = (torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16()
+    dz = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
+    xr, wr = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)
+    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
+    prev = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
+    dx = prev.clone()
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
+                                  K=KH * KW * Fo, flags=H.GF_ACCUM, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)], "v3")
+    ref = prev.float() + torch.nn.grad.conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    assert _rel(dx.float(), ref) < 6e-3
+    prev_y = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
+    y = prev_y.clone()
+    _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), M=B * OH * OW, N=Fo,
+                                K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)], "v3")
+    ref_y = prev_y.float() + F.conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)
+    assert _rel(y.float(), ref_y) < 6e-3
