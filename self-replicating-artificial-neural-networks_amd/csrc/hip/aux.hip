@@ -147,12 +147,218 @@ __device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const 
     var = fmaxf(ws[C + c] / R - m1 * m1, 0.f);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Vectorised BatchNormalizationF16 for C <= 256 (every BN of a SeRANN: X/g channels <= 128, merged
+// units <= 256).  The [R][C] tensor is walked in "super-rows" of 8 rows = C chunks of 8 elements, so
+// a thread that always takes chunk i of a super-row always sees the same 8 channels
+// ((8i + j) mod C): 16-B loads/stores, per-thread registers for the 8 channels' parameters and
+// partial sums, per-channel combination through LDS float atomics, one global atomic per channel
+// and block.  Works for any C (odd channel counts included).
+constexpr int BN_VEC_ELEMS = 16384;     // elements per block (super-rows per block = 2048 / C)
+
+__device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, float* sA, float* sB) {
+    const int R = (int)d.R, C = (int)d.C;
+    const int flags = (int)d.flags;
+    const float eps = (float)d.eps;
+    const float Rf = (float)R;
+    const int t = threadIdx.x;
+    const int G = 256 / C;                       // super-rows processed together
+    const bool active = t < G * C;
+    const int q = t / C, i = t - q * C;
+    const int srb = max(1, (BN_VEC_ELEMS / 8) / C);
+    const int nsr = (R + 7) / 8;
+    const int sr0 = tile * srb, sr1 = min(nsr, sr0 + srb);
+    const int64_t total = (int64_t)R * C;
+    const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
+    float* ws = reinterpret_cast<float*>(d.ws);
+    int ch[8];
+    {
+        int c = (8 * i) % C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { ch[j] = c; c = (c + 1 == C) ? 0 : c + 1; }
+    }
+    // per-channel parameters into LDS (sA: scale-like, sB: shift-like)
+    for (int c = t; c < C; c += 256) {
+        float a = 0.f, b = 0.f;
+        if (phase == 0) {
+            a = bf2f(x[c]);                                    // shift K_c = x[0][c]
+        } else if (phase == 2 || phase == 3) {
+            float mu, var;
+            if (phase == 2) {
+                const float K = bf2f(x[c]);
+                const float m1 = ws[c] / Rf;
+                mu = K + m1;
+                var = fmaxf(ws[C + c] / Rf - m1 * m1, 0.f);
+            } else {
+                mu = reinterpret_cast<const float*>(d.mm)[c];
+                var = reinterpret_cast<const float*>(d.mv)[c];
+            }
+            const float is = rsqrtf(var + eps);
+            const float gsc = (flags & 1) ? reinterpret_cast<const float*>(d.gamma)[c] * is : is;
+            a = gsc;
+            b = ((flags & 2) ? reinterpret_cast<const float*>(d.beta)[c] : 0.f) - mu * gsc;
+        } else if (phase == 4) {
+            a = reinterpret_cast<const float*>(d.mean)[c];
+            b = reinterpret_cast<const float*>(d.invstd)[c];
+        } else {   // phase 5: dx = gg * (dy - ma - (x - mu) * is * mb) = k1 * dy + k2 * x + k3
+            const float mu = reinterpret_cast<const float*>(d.mean)[c];
+            const float is = reinterpret_cast<const float*>(d.invstd)[c];
+            const float gg = ((flags & 1) ? reinterpret_cast<const float*>(d.gamma)[c] : 1.f) * is;
+            const float ma = ws[c] / Rf, mb = ws[C + c] / Rf;
+            a = gg;                                            // k1
+            b = -gg * is * mb;                                 // k2
+            sA[256 + c] = -gg * (ma - mu * is * mb);           // k3
+        }
+        sA[c] = a;
+        sB[c] = b;
+    }
+    if (phase == 2 && tile == 0) {
+        const float mom = (float)d.momentum;
+        float* mm = reinterpret_cast<float*>(d.mm);
+        float* mv = reinterpret_cast<float*>(d.mv);
+        float* mean = reinterpret_cast<float*>(d.mean);
+        float* invstd = reinterpret_cast<float*>(d.invstd);
+        for (int c = t; c < C; c += 256) {
+            const float K = bf2f(x[c]);
+            const float m1 = ws[c] / Rf;
+            const float mu = K + m1;
+            const float var = fmaxf(ws[C + c] / Rf - m1 * m1, 0.f);
+            mm[c] = mm[c] * mom + mu * (1.f - mom);
+            mv[c] = mv[c] * mom + var * (Rf / (Rf - (1.f + eps))) * (1.f - mom);
+            mean[c] = mu;
+            invstd[c] = rsqrtf(var + eps);
+        }
+    }
+    if (phase == 5 && tile == 0) {
+        for (int c = t; c < C; c += 256) {
+            if (flags & 1) reinterpret_cast<float*>(d.dgamma)[c] += ws[C + c];
+            if (flags & 2) reinterpret_cast<float*>(d.dbeta)[c] += ws[c];
+        }
+    }
+    __syncthreads();
+    float pa[8], pb[8], p3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        pa[j] = sA[ch[j]];
+        pb[j] = sB[ch[j]];
+        p3[j] = (phase == 5) ? sA[256 + ch[j]] : 0.f;
+    }
+    __syncthreads();
+    const bool reduce = phase == 0 || phase == 4;
+    if (phase == 5 && (flags & 8)) return;
+    float acc0[8], acc1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acc0[j] = 0.f; acc1[j] = 0.f; }
+    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+    bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
+    bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
+    if (active) {
+        // 4 super-rows per iteration: all loads are issued before any use (memory-level parallelism)
+        constexpr int U = 4;
+        for (int sr = sr0 + q; sr < sr1; sr += U * G) {
+            union V8 { uint4 u; bf16_t h[8]; };
+            V8 xv[U], gv[U], old[U];
+            int64_t e[U];
+            int nv[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int s_ = sr + k * G;
+                e[k] = (int64_t)s_ * 8 * C + 8 * i;
+                nv[k] = s_ < sr1 ? (int)max((int64_t)0, min((int64_t)8, total - e[k])) : 0;
+                xv[k].u = make_uint4(0, 0, 0, 0);
+                gv[k].u = make_uint4(0, 0, 0, 0);
+                old[k].u = make_uint4(0, 0, 0, 0);
+                if (nv[k] == 8) {
+                    xv[k].u = *reinterpret_cast<const uint4*>(x + e[k]);
+                    if (phase >= 4) gv[k].u = *reinterpret_cast<const uint4*>(dy + e[k]);
+                    if (phase == 5 && (flags & 4)) old[k].u = *reinterpret_cast<const uint4*>(dx + e[k]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {           // static indices: stays in registers
+                        if (j < nv[k]) {
+                            xv[k].h[j] = x[e[k] + j];
+                            if (phase >= 4) gv[k].h[j] = dy[e[k] + j];
+                            if (phase == 5 && (flags & 4)) old[k].h[j] = dx[e[k] + j];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                if (nv[k] <= 0) continue;
+                V8 ov;
+                if (phase == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j < nv[k]) { const float v = bf2f(xv[k].h[j]) - pa[j]; acc0[j] += v; acc1[j] += v * v; }
+                    continue;
+                }
+                if (phase == 4) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float g = bf2f(gv[k].h[j]);
+                        acc0[j] += g;
+                        acc1[j] += g * (bf2f(xv[k].h[j]) - pa[j]) * pb[j];
+                    }
+                    continue;
+                }
+                bf16_t* dst = (phase == 5) ? dx : y;
+                if (phase == 5) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        ov.h[j] = f2bf(pa[j] * bf2f(gv[k].h[j]) + pb[j] * bf2f(xv[k].h[j]) + p3[j] + bf2f(old[k].h[j]));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ov.h[j] = f2bf(bf2f(xv[k].h[j]) * pa[j] + pb[j]);
+                }
+                if (nv[k] == 8) {
+                    *reinterpret_cast<uint4*>(dst + e[k]) = ov.u;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j < nv[k]) dst[e[k] + j] = ov.h[j];
+                }
+            }
+        }
+    }
+    if (reduce) {
+        // slot (q, 8i + j) holds channel (8i + j) mod C of super-row group q; channel c owns the
+        // slots c, c + C, ..., c + 7C of every group -- a gather instead of LDS atomics
+        float* r0 = sA;
+        float* r1 = sA + 2048;
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                r0[q * 8 * C + 8 * i + j] = acc0[j];
+                r1[q * 8 * C + 8 * i + j] = acc1[j];
+            }
+        }
+        __syncthreads();
+        for (int c = t; c < C; c += 256) {
+            float a = 0.f, b = 0.f;
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    a += r0[g * 8 * C + c + k * C];
+                    b += r1[g * 8 * C + c + k * C];
+                }
+            atomicAdd(&ws[c], a);
+            atomicAdd(&ws[C + c], b);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ descs, const int2* __restrict__ tiles,
                                                  int phase) {
-    __shared__ float s0[256];
+    __shared__ float s0[4096];           // vectorised path: 2 x (G * 8 * C <= 2048) reduction slots
     __shared__ float s1[256];
     const int2 td = tiles[blockIdx.x];
     const BnDesc& d = descs[td.x];
+    if (d.C <= 256) {
+        bn_vec(d, td.y, phase, s0, s1);
+        return;
+    }
     const int R = (int)d.R, C = (int)d.C;
     const int flags = (int)d.flags;
     const float eps = (float)d.eps;
@@ -262,66 +468,126 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
 // windows covering each input element (handles overlapping windows from explicit strides).
 constexpr int POOL_ELEMS = 1024;
 
-__global__ __launch_bounds__(256) void pool_fwd_kernel(const PoolDesc* __restrict__ descs, const int2* __restrict__ tiles) {
-    const int2 td = tiles[blockIdx.x];
-    const PoolDesc& d = descs[td.x];
+// A work unit is V consecutive channels of one pixel: V = 8 (16-B vectors, 8-B argmax bytes) when
+// C % 8 == 0 -- every pooled conv output, whose filter counts are powers of two -- else V = 1.  Index
+// math is 32-bit (the tensors of one organism stay far below 2^31 elements).
+__device__ __forceinline__ int pool_vec(int C) { return (C & 7) == 0 ? 8 : 1; }
+
+template <int V>
+__device__ __forceinline__ void pool_fwd_units(const PoolDesc& d, int u0, int u1) {
     const int C = (int)d.C, OW = (int)d.OW, OH = (int)d.OH, W = (int)d.W, H = (int)d.H;
     const int PH = (int)d.PH, PW = (int)d.PW, SH = (int)d.SH, SW = (int)d.SW;
-    const int64_t total = d.B * OH * OW * C;
-    const bf16_t* x = reinterpret_cast<const bf16_t*>(d.x);
-    bf16_t* y = reinterpret_cast<bf16_t*>(d.y);
-    uint8_t* idx = reinterpret_cast<uint8_t*>(d.idx);
-    const int64_t e0 = (int64_t)td.y * POOL_ELEMS;
-    for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + POOL_ELEMS); e += blockDim.x) {
-        int64_t t = e;
-        const int c = t % C; t /= C;
-        const int ow = t % OW; t /= OW;
-        const int oh = t % OH;
-        const int64_t b = t / OH;
-        float best = -INFINITY;
-        int bi = 0;
+    const int CV = C / V;
+    const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
+    bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
+    uint8_t* __restrict__ idx = reinterpret_cast<uint8_t*>(d.idx);
+    for (int u = u0 + (int)threadIdx.x; u < u1; u += blockDim.x) {
+        const int pix = u / CV;
+        const int c = (u - pix * CV) * V;
+        const int b = pix / (OH * OW);
+        const int r = pix - b * (OH * OW);
+        const int oh = r / OW, ow = r - (r / OW) * OW;
+        float best[V];
+        uint8_t bi[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) { best[j] = -INFINITY; bi[j] = 0; }
         for (int i = 0; i < PH; ++i)
-            for (int j = 0; j < PW; ++j) {
-                const float v = bf2f(x[((b * H + oh * SH + i) * W + ow * SW + j) * C + c]);
-                if (v > best || (v != v && best == best)) { best = v; bi = i * PW + j; }
+            for (int jj = 0; jj < PW; ++jj) {
+                const int off = ((b * H + oh * SH + i) * W + ow * SW + jj) * C + c;
+                union { uint4 u; bf16_t h[8]; } xv;
+                if (V == 8) xv.u = *reinterpret_cast<const uint4*>(x + off);
+                else xv.h[0] = x[off];
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const float v = bf2f(xv.h[j]);
+                    if (v > best[j] || (v != v && best[j] == best[j])) { best[j] = v; bi[j] = (uint8_t)(i * PW + jj); }
+                }
             }
-        y[e] = f2bf(best);
-        idx[e] = (uint8_t)bi;
+        const int o = pix * C + c;
+        if (V == 8) {
+            union { uint4 u; bf16_t h[8]; } ov;
+            union { uint2 u; uint8_t b[8]; } iv;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { ov.h[j] = f2bf(best[j]); iv.b[j] = bi[j]; }
+            *reinterpret_cast<uint4*>(y + o) = ov.u;
+            *reinterpret_cast<uint2*>(idx + o) = iv.u;
+        } else {
+            y[o] = f2bf(best[0]);
+            idx[o] = bi[0];
+        }
     }
 }
 
-__global__ __launch_bounds__(256) void pool_bwd_kernel(const PoolDesc* __restrict__ descs, const int2* __restrict__ tiles) {
-    const int2 td = tiles[blockIdx.x];
-    const PoolDesc& d = descs[td.x];
+template <int V>
+__device__ __forceinline__ void pool_bwd_units(const PoolDesc& d, int u0, int u1) {
     const int C = (int)d.C, OW = (int)d.OW, OH = (int)d.OH, W = (int)d.W, H = (int)d.H;
     const int PH = (int)d.PH, PW = (int)d.PW, SH = (int)d.SH, SW = (int)d.SW;
-    const int64_t total = d.B * H * W * C;
-    const bf16_t* dy = reinterpret_cast<const bf16_t*>(d.dy);
-    bf16_t* dx = reinterpret_cast<bf16_t*>(d.dx);
-    const uint8_t* idx = reinterpret_cast<const uint8_t*>(d.idx);
-    const int64_t e0 = (int64_t)td.y * POOL_ELEMS;
-    for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + POOL_ELEMS); e += blockDim.x) {
-        int64_t t = e;
-        const int c = t % C; t /= C;
-        const int iw = t % W; t /= W;
-        const int ih = t % H;
-        const int64_t b = t / H;
-        float acc = 0.f;
+    const int CV = C / V;
+    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+    bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
+    const uint8_t* __restrict__ idx = reinterpret_cast<const uint8_t*>(d.idx);
+    for (int u = u0 + (int)threadIdx.x; u < u1; u += blockDim.x) {
+        const int pix = u / CV;
+        const int c = (u - pix * CV) * V;
+        const int b = pix / (H * W);
+        const int r = pix - b * (H * W);
+        const int ih = r / W, iw = r - (r / W) * W;
+        float acc[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = 0.f;
         const int oh_lo = max(0, (ih - PH + SH) / SH), oh_hi = min(OH - 1, ih / SH);
         const int ow_lo = max(0, (iw - PW + SW) / SW), ow_hi = min(OW - 1, iw / SW);
         for (int oh = oh_lo; oh <= oh_hi; ++oh) {
             const int i = ih - oh * SH;
             if (i < 0 || i >= PH) continue;
             for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-                const int j = iw - ow * SW;
-                if (j < 0 || j >= PW) continue;
-                const int64_t o = ((b * OH + oh) * OW + ow) * C + c;
-                if (idx[o] == i * PW + j) acc += bf2f(dy[o]);
+                const int jj = iw - ow * SW;
+                if (jj < 0 || jj >= PW) continue;
+                const uint8_t want = (uint8_t)(i * PW + jj);
+                const int o = ((b * OH + oh) * OW + ow) * C + c;
+                union { uint4 u; bf16_t h[8]; } gv;
+                union { uint2 u; uint8_t b[8]; } iv;
+                if (V == 8) { gv.u = *reinterpret_cast<const uint4*>(dy + o); iv.u = *reinterpret_cast<const uint2*>(idx + o); }
+                else { gv.h[0] = dy[o]; iv.b[0] = idx[o]; }
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    if (iv.b[j] == want) acc[j] += bf2f(gv.h[j]);
             }
         }
-        if (d.flags & 1) acc += bf2f(dx[e]);
-        dx[e] = f2bf(acc);
+        const int e = pix * C + c;
+        if (V == 8) {
+            union { uint4 u; bf16_t h[8]; } ov, old;
+            if (d.flags & 1) old.u = *reinterpret_cast<const uint4*>(dx + e);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ov.h[j] = f2bf(acc[j] + ((d.flags & 1) ? bf2f(old.h[j]) : 0.f));
+            *reinterpret_cast<uint4*>(dx + e) = ov.u;
+        } else {
+            float v = acc[0];
+            if (d.flags & 1) v += bf2f(dx[e]);
+            dx[e] = f2bf(v);
+        }
     }
+}
+
+// one block = POOL_ELEMS work units (units of V channels; tiles from hip_ops.pool_units)
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const PoolDesc* __restrict__ descs, const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const PoolDesc& d = descs[td.x];
+    const int V = pool_vec((int)d.C);
+    const int total = (int)(d.B * d.OH * d.OW * d.C / V);
+    const int u0 = td.y * POOL_ELEMS, u1 = min(total, u0 + POOL_ELEMS);
+    if (V == 8) pool_fwd_units<8>(d, u0, u1);
+    else pool_fwd_units<1>(d, u0, u1);
+}
+
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const PoolDesc* __restrict__ descs, const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const PoolDesc& d = descs[td.x];
+    const int V = pool_vec((int)d.C);
+    const int total = (int)(d.B * d.H * d.W * d.C / V);
+    const int u0 = td.y * POOL_ELEMS, u1 = min(total, u0 + POOL_ELEMS);
+    if (V == 8) pool_bwd_units<8>(d, u0, u1);
+    else pool_bwd_units<1>(d, u0, u1);
 }
 
 // ------------------------------------------------------------------------------------------------

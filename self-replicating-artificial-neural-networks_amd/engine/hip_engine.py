@@ -576,7 +576,7 @@ class HipPopulationEngine(PopulationEngine):
                                            y=self._act_ptr(mem, o, n.id, inputs),
                                            idx=mem["u8"].ptr(rec["idx"][n.id]), B=B, H=a["h"], W=a["w"], C=a["c"],
                                            OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"]))
-                        p_cnt.append(B * math.prod(n.shape))
+                        p_cnt.append(H.pool_units(B * math.prod(n.shape), a["c"]))
                     elif n.op == "bn" and a["last"]:
                         bd = rec["bn"][n.id]
                         c = a["channels"]
@@ -589,7 +589,7 @@ class HipPopulationEngine(PopulationEngine):
                                             mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
                                             ws=mem["ws"].ptr(bd["ws"]), R=B * math.prod(n.shape) // c, C=c,
                                             flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
-                        bn_cnt.append(H.red_chunks(B * math.prod(n.shape) // c, c))
+                        bn_cnt.append(H.bn_chunks(B * math.prod(n.shape) // c, c))
                     elif n.op == "concat":
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])
@@ -745,7 +745,7 @@ class HipPopulationEngine(PopulationEngine):
                                         dx=mem["grad"].ptr(rec["grad"][own]), B=B, H=a["h"], W=a["w"], C=a["c"],
                                         OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"])
                             tasks["pool"].append((o, own, lambda acc, r=base: dict(r, flags=1 if acc else 0),
-                                                  B * a["h"] * a["w"] * a["c"]))
+                                                  H.pool_units(B * a["h"] * a["w"] * a["c"], a["c"])))
                     elif n.op == "bn" and a["last"]:
                         bd = rec["bn"][n.id]
                         c = a["channels"]
@@ -762,13 +762,13 @@ class HipPopulationEngine(PopulationEngine):
                                     dbeta=gptr(lay.beta[n.id]) if n.id in lay.beta else 0,
                                     R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
                         bn_red.append(dict(base, flags=pflags))
-                        bn_red_cnt.append(H.red_chunks(R, c))
+                        bn_red_cnt.append(H.bn_chunks(R, c))
                         if own is None:
                             tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
-                                                H.red_chunks(R, c)))
+                                                H.bn_chunks(R, c)))
                         else:
                             tasks["bn"].append((o, own, lambda acc, r=base, f=pflags: dict(r, flags=f | (4 if acc else 0)),
-                                                H.red_chunks(R, c)))
+                                                H.bn_chunks(R, c)))
                     elif n.op == "concat":
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])

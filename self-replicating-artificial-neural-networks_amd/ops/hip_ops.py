@@ -70,6 +70,23 @@ def gemm_desc_array(rows) -> np.ndarray:
     return fill_gemm_divisors(a)
 
 
+BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256) BatchNorm kernel
+
+
+def bn_chunks(rows: int, channels: int) -> int:
+    """Blocks of a BatchNorm problem [rows][channels] (aux.hip bn_kernel chunking)."""
+    c = max(int(channels), 1)
+    if c > 256:
+        return red_chunks(rows, c)
+    srb = max(1, (BN_VEC_ELEMS // 8) // c)
+    return -(-(-(-int(rows) // 8)) // srb)
+
+
+def pool_units(elements: int, channels: int) -> int:
+    """Work units of a MaxPool problem (aux.hip: 8-channel vectors when C % 8 == 0)."""
+    return int(elements) // (8 if int(channels) % 8 == 0 else 1)
+
+
 def red_chunks(rows: int, channels: int) -> int:
     """Blocks needed by a BN / act_bwd problem of shape [rows][channels]."""
     per = max(1, RED_ELEMS // max(int(channels), 1))

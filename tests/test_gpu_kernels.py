@@ -147,8 +147,9 @@ def test_grouped_gemm_many_problems_one_launch(impl):
         assert _rel(y.float(), r) < 6e-3
 
 
-def test_bn_train_infer_backward():
-    R, C = 3000, 13
+@pytest.mark.parametrize("RC", [(3000, 13), (20001, 67), (4096, 256), (999, 300)])
+def test_bn_train_infer_backward(RC):
+    R, C = RC
     x = (torch.randn(R, C, device=DEV) * 3 + 1).bfloat16()
     gamma = torch.rand(C, device=DEV) + 0.5
     beta = torch.randn(C, device=DEV)
@@ -163,7 +164,7 @@ def test_bn_train_infer_backward():
                beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(), invstd=invstd.data_ptr(),
                ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
     d = _desc([row], H.BN_DTYPE)
-    t = torch.as_tensor(H.chunk_tiles([H.red_chunks(R, C)], 1), device=DEV)
+    t = torch.as_tensor(H.chunk_tiles([H.bn_chunks(R, C)], 1), device=DEV)
     L, s = H.lib(), H.stream_handle()
     for ph in (0, 2):
         L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
@@ -191,10 +192,12 @@ def test_bn_train_infer_backward():
     assert _rel(y.float(), ref_inf) < 6e-3
 
 
+@pytest.mark.parametrize("C", [5, 16])
 @pytest.mark.parametrize("p", [(2, 2, 2, 2), (3, 3, 3, 3), (3, 3, 2, 2), (2, 3, 1, 2)])
-def test_maxpool_fwd_bwd(p):
+def test_maxpool_fwd_bwd(p, C):
+    """C=5: element units; C=16: 8-channel vector units (aux.hip pool_vec)."""
     PH, PW, SH, SW = p
-    B, Hh, Ww, C = 3, 13, 11, 5
+    B, Hh, Ww = 3, 13, 11
     OH, OW = (Hh - PH) // SH + 1, (Ww - PW) // SW + 1
     x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
     y = torch.zeros(B, OH, OW, C, dtype=torch.bfloat16, device=DEV)
@@ -205,9 +208,9 @@ def test_maxpool_fwd_bwd(p):
                C=C, OH=OH, OW=OW, PH=PH, PW=PW, SH=SH, SW=SW, flags=0)
     d = _desc([row], H.POOL_DTYPE)
     L, s = H.lib(), H.stream_handle()
-    t = torch.as_tensor(H.chunk_tiles([B * OH * OW * C], H.POOL_ELEMS), device=DEV)
+    t = torch.as_tensor(H.chunk_tiles([H.pool_units(B * OH * OW * C, C)], H.POOL_ELEMS), device=DEV)
     L.pool(0, d.data_ptr(), t.data_ptr(), len(t), s)
-    t2 = torch.as_tensor(H.chunk_tiles([B * Hh * Ww * C], H.POOL_ELEMS), device=DEV)
+    t2 = torch.as_tensor(H.chunk_tiles([H.pool_units(B * Hh * Ww * C, C)], H.POOL_ELEMS), device=DEV)
     L.pool(1, d.data_ptr(), t2.data_ptr(), len(t2), s)
     torch.cuda.synchronize()
     xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
