@@ -997,12 +997,164 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     }
 }
 
+// ==================================================================================================
+// Narrow layers: 1x1 / Dense problems with K <= 4 reduction channels (X_Dense on the raw image, or on a
+// conv output with 1-4 filters).  There is nothing for MFMA to do -- K is 1..4 -- and the work is pure
+// streaming of the wide [M][N] tensor, so these are VALU kernels with 16-B accesses: a thread keeps 8
+// consecutive output channels (their K weights / gradient partial sums in registers) and walks rows.
+constexpr int NARROW_ROWS = 256;        // FWD rows per block
+constexpr int NARROW_WROWS = 1024;      // WGRAD rows per block
+
+template <int K>
+__global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __restrict__ descs,
+                                                            const int4* __restrict__ tiles) {
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const int M = (int)d.M, N = (int)d.N, act = (int)d.act;
+    const int ldx = (int)d.C;                    // X row stride (= K, or K8 for the shared raw im2col)
+    const int FC = (N + 7) >> 3;                 // 8-channel chunks per row (<= 32: N <= 256)
+    const int RPI = 256 / FC;
+    const int t = threadIdx.x;
+    if (t >= RPI * FC) return;
+    const int chunk = t % FC, rl = t / FC;
+    const int f0 = chunk * 8;
+    const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.a);
+    const bf16_t* __restrict__ Wm = reinterpret_cast<const bf16_t*>(d.b);
+    const float* bias = reinterpret_cast<const float*>(d.bias);
+    bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(d.out);
+    float w[8][K], bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int f = min(f0 + j, N - 1);
+        bv[j] = bias ? bias[f] : 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) w[j][k] = bf2f(Wm[f * K + k]);
+    }
+    const bool vec = (N & 7) == 0;
+    const int r0 = td.y * NARROW_ROWS, r1 = min(M, r0 + NARROW_ROWS);
+    constexpr int U = 4;                         // rows in flight per thread
+    for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
+        float xv[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = min(rb + u * RPI, r1 - 1);
+#pragma unroll
+            for (int k = 0; k < K; ++k) xv[u][k] = bf2f(X[(int64_t)r * ldx + k]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rb + u * RPI;
+            if (r >= r1) break;
+            union { uint4 u4; bf16_t h[8]; } o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v = bv[j];
+#pragma unroll
+                for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
+                o.h[j] = f2bf(apply_act(v, act));
+            }
+            bf16_t* dst = Y + (int64_t)r * N + f0;
+            if (vec) {
+                *reinterpret_cast<uint4*>(dst) = o.u4;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (f0 + j < N) dst[j] = o.h[j];
+            }
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                              const int4* __restrict__ tiles) {
+    // WGRAD dims: M = F (rows of dW), N = K (columns), K = reduction rows; dZ = dY * act'(Y)
+    constexpr int NA = 8 * (K + 1);               // per-thread partials: 8 x K weights + 8 biases
+    __shared__ float red[256 * NA];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const int F = (int)d.M, R = (int)d.K, act = (int)d.act;
+    const int ldx = (int)d.C;                    // X row stride (= K, or K8 for the shared raw im2col)
+    const int FC = (F + 7) >> 3;
+    const int RPI = 256 / FC;
+    const int t = threadIdx.x;
+    const bool active = t < RPI * FC;
+    const int chunk = t % FC, rl = t / FC;
+    const int f0 = chunk * 8;
+    const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
+    const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
+    const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
+    float* dbias = reinterpret_cast<float*>(d.bias);
+    float acc[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) acc[j] = 0.f;
+    const bool vec = (F & 7) == 0;
+    const int r0 = td.y * NARROW_WROWS, r1 = min(R, r0 + NARROW_WROWS);
+    if (active) {
+        constexpr int U = 4;                     // rows in flight per thread
+        for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
+            union V8 { uint4 u; bf16_t h[8]; };
+            V8 g[U], y[U];
+            float xv[U][K];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = rb + u * RPI;
+                const bool ok = r < r1;
+                const int rr = ok ? r : r0;
+                const bf16_t* src = dY + (int64_t)rr * F + f0;
+                const bf16_t* ysrc = Yv + (int64_t)rr * F + f0;
+                if (vec) {
+                    g[u].u = *reinterpret_cast<const uint4*>(src);
+                    if (act != ACT_LINEAR) y[u].u = *reinterpret_cast<const uint4*>(ysrc);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        g[u].h[j] = f0 + j < F ? src[j] : (bf16_t)0;
+                        if (act != ACT_LINEAR) y[u].h[j] = f0 + j < F ? ysrc[j] : (bf16_t)0;
+                    }
+                }
+                if (!ok) g[u].u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int k = 0; k < K; ++k) xv[u][k] = bf2f(X[(int64_t)rr * ldx + k]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float gz = bf2f(g[u].h[j]);
+                    if (act != ACT_LINEAR) gz = bf2f(f2bf(gz * act_grad_from_y(bf2f(y[u].h[j]), act)));
+#pragma unroll
+                    for (int k = 0; k < K; ++k) acc[j * K + k] += gz * xv[u][k];
+                    acc[8 * K + j] += gz;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) red[j * 256 + t] = active ? acc[j] : 0.f;
+    __syncthreads();
+    // combine the RPI row lanes of every (chunk, partial) and flush
+    for (int o = t; o < FC * NA; o += 256) {
+        const int ch = o / NA, j = o - ch * NA;
+        float v = 0.f;
+        for (int q = 0; q < RPI; ++q) v += red[j * 256 + q * FC + ch];
+        if (j < 8 * K) {
+            const int f = ch * 8 + j / K, k = j % K;
+            if (f < F) atomicAdd(reinterpret_cast<float*>(d.out) + (int64_t)f * K + k, v);
+        } else {
+            const int f = ch * 8 + (j - 8 * K);
+            if (dbias && f < F) atomicAdd(dbias + f, v);
+        }
+    }
+}
+
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
-//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form
+//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4)
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
 // variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
+//                 narrow (K <= 4): 4000000 + K; tiles (prob, row block, 0, 0)
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
 //                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
@@ -1011,6 +1163,16 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
     const int4* tp = as_ptr<const int4>(tiles);
     dim3 grid((unsigned)ntiles), block(256);
+    if (mode == MODE_WGRAD && variant >= 4000000) {
+        const int k = variant - 4000000;
+        if (k == 1) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<1>), grid, block, 0, s, dp, tp);
+        else if (k == 2) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<2>), grid, block, 0, s, dp, tp);
+        else if (k == 3) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<3>), grid, block, 0, s, dp, tp);
+        else if (k == 4) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<4>), grid, block, 0, s, dp, tp);
+        else throw std::runtime_error("gemm3: unknown narrow WGRAD variant " + std::to_string(variant));
+        SERANN_CHECK(hipGetLastError());
+        return;
+    }
     if (mode == MODE_WGRAD && variant >= 3000000) {
         const int tier = (variant / 100000) % 10;
         const int v = variant % 100000;
@@ -1051,6 +1213,16 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef C3T
 #undef C3
         throw std::runtime_error("gemm3: unknown conv variant " + std::to_string(variant));
+    }
+    if (mode == MODE_FWD && variant >= 6000) {
+        const int k = variant - 6000;
+        if (k == 1) hipLaunchKernelGGL((g3_narrow_fwd_kernel<1>), grid, block, 0, s, dp, tp);
+        else if (k == 2) hipLaunchKernelGGL((g3_narrow_fwd_kernel<2>), grid, block, 0, s, dp, tp);
+        else if (k == 3) hipLaunchKernelGGL((g3_narrow_fwd_kernel<3>), grid, block, 0, s, dp, tp);
+        else if (k == 4) hipLaunchKernelGGL((g3_narrow_fwd_kernel<4>), grid, block, 0, s, dp, tp);
+        else throw std::runtime_error("gemm3: unknown narrow FWD variant " + std::to_string(variant));
+        SERANN_CHECK(hipGetLastError());
+        return;
     }
     if (variant >= 5000) {
         const int v = variant - 5000;

@@ -164,7 +164,7 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
         return bmf * 1000 + bnk + (1000000 if im2col_gen else 0)
     gen = im2col_gen if mode == MODE_FWD else (F % 8 != 0 and KH * KW > 1)
     nt = 1 if N <= 16 else (2 if N <= 32 else (4 if N <= 64 else 8))
-    if K <= 32 and not gen and M >= 16384:       # single k step: store-bound, keep registers low
+    if K <= 32 and not gen and M >= 16384 and "sk" not in _OFF:       # single k step: store-bound, keep registers low
         return 5000 + nt + 10 * (2 if nt == 8 else 4)
     kw = M <= 8192 and -(-K // BK) >= 16
     rt = 2 if (kw or nt == 8 or M < 16384) else 4
@@ -192,7 +192,7 @@ def conv_lds_config(geo: dict, N: int):
     per-image pixel count stays within 20% of the smallest tiling, then the smallest patch tier that
     holds it (more blocks resident per CU)."""
     KH, KW, C, W, OH, OW, SH = (int(geo[k]) for k in ("KH", "KW", "C", "W", "OH", "OW", "SH"))
-    if KH * KW <= 1:
+    if KH * KW <= 1 or "conv_fwd" in _OFF:
         return None
     cp = -(-C // 8) * 8
     cs = cp if (cp // 8) % 2 == 1 else cp + 8
@@ -213,7 +213,7 @@ def conv_lds_config(geo: dict, N: int):
 def conv_wgrad_config(geo: dict, F: int):
     """(BMF, BNK, patch tier) for the LDS-halo conv WGRAD kernel (128-pixel chunks), or None."""
     KH, KW, C, W, OH, OW, SH = (int(geo[k]) for k in ("KH", "KW", "C", "W", "OH", "OW", "SH"))
-    if KH * KW <= 1:
+    if KH * KW <= 1 or "conv_wgrad" in _OFF:
         return None
     cp = -(-C // 8) * 8
     cs = cp if (cp // 8) % 2 == 1 else cp + 8
@@ -231,6 +231,27 @@ def conv_wgrad_config(geo: dict, F: int):
     return bmf, bnk, tier
 
 
+NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
+
+import os as _os
+# A/B switches for measurements and fault isolation (all paths are on by default)
+_OFF = set(filter(None, _os.environ.get("SERANN_GEMM3_OFF", "").split(",")))   # conv_fwd,conv_wgrad,narrow,sk
+
+
+def narrow_k(geo: dict, mode: int, M: int, N: int, K: int):
+    """Reduction width of a 1x1 / Dense problem that the narrow VALU kernels take (K <= 4, N <= 256,
+    no stride, no accumulate), else None."""
+    if int(geo.get("KH", 1)) * int(geo.get("KW", 1)) != 1 or int(geo.get("SH", 1)) * int(geo.get("SW", 1)) != 1:
+        return None
+    if int(geo.get("flags", 0)) & (GF_ACCUM | GF_OUT_F32) or "narrow" in _OFF:
+        return None
+    if mode == MODE_FWD and K <= 4 and N <= 256:
+        return K
+    if mode == MODE_WGRAD and N <= 4 and M <= 256:
+        return N
+    return None
+
+
 def gemm3_plan(mode: int, rows, dims):
     """Group the problems of one grouped launch by v3 kernel instantiation.
 
@@ -241,12 +262,15 @@ def gemm3_plan(mode: int, rows, dims):
     for r, dm in zip(rows, dims):
         M, N, K = dm
         v = None
-        if mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
+        nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) else None
+        if nk is not None:
+            v = (6000 if mode == MODE_FWD else 4000000) + nk
+        elif mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
             cfg = conv_lds_config(r, N)
             if cfg is not None:
                 nt = 1 if N <= 16 else (2 if N <= 32 else 4)
                 v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
-        if mode == MODE_WGRAD:
+        if mode == MODE_WGRAD and v is None:
             cfg = conv_wgrad_config(r, M)
             if cfg is not None:
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
@@ -256,7 +280,15 @@ def gemm3_plan(mode: int, rows, dims):
     out = []
     for v in sorted(groups):
         items = groups[v]
-        if 2000 <= v < 3000 and mode == MODE_FWD:
+        if (mode == MODE_FWD and v >= 6000) or (mode == MODE_WGRAD and v >= 4000000):
+            per = NARROW_ROWS if mode == MODE_FWD else NARROW_WROWS
+            tl = []
+            for p, (r, (M, N, K)) in enumerate(items):
+                nrows = M if mode == MODE_FWD else K
+                nb = -(-nrows // per)
+                tl.append(np.stack([np.full(nb, p), np.arange(nb), np.zeros(nb, int), np.zeros(nb, int)], 1))
+            tiles = np.concatenate(tl).astype(np.int32)
+        elif 2000 <= v < 3000 and mode == MODE_FWD:
             nt, rt = v % 10, (v // 10) % 10
             tm, bn = 64 * rt, 16 * nt
             tl = []

@@ -72,6 +72,9 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     # single-k-step FWD/DGRAD (K <= 32, M >= 16384) and the narrow (N <= 16) WGRAD layout
     (30, 28, 28, 1, 100, 1, 1, 1, 1, "relu"),
     (25, 26, 26, 24, 40, 1, 1, 1, 1, "sigmoid"),
+    # narrow VALU kernels (K <= 4 input channels, 1x1): FWD and WGRAD
+    (4, 9, 9, 3, 200, 1, 1, 1, 1, "sigmoid"),
+    (6, 10, 10, 2, 13, 1, 1, 1, 1, "linear"),
 ]
 
 
@@ -147,7 +150,7 @@ def test_grouped_gemm_many_problems_one_launch(impl):
         assert _rel(y.float(), r) < 6e-3
 
 
-@pytest.mark.parametrize("RC", [(3000, 13), (20001, 67), (4096, 256), (999, 300)])
+@pytest.mark.parametrize("RC", [(3000, 13), (20001, 67), (4096, 256), (999, 300), (5000, 1), (3001, 3)])
 def test_bn_train_infer_backward(RC):
     R, C = RC
     x = (torch.randn(R, C, device=DEV) * 3 + 1).bfloat16()
@@ -244,12 +247,15 @@ def test_loss_kernel_matches_keras_losses():
     assert abs(metrics[2].item() / B - mse.item()) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(3, 9, 9, 8, 13, 3, 3), (3, 9, 9, 2, 13, 1, 1), (50, 12, 12, 1, 70, 1, 1)])
 @pytest.mark.parametrize("impl", ["v2", "v3"])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
-def test_fused_act_grad_and_bias_grad(act, impl):
-    """v2/v3 WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient."""
-    B, Hh, Ww, C, Fo, KH, KW, SH, SW = 3, 9, 9, 8, 13, 3, 3, 1, 1
-    OH, OW = Hh - 2, Ww - 2
+def test_fused_act_grad_and_bias_grad(act, impl, shape):
+    """v2/v3 WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient
+    (1x1 shapes with C <= 4 take the v3 narrow VALU kernels)."""
+    B, Hh, Ww, C, Fo, KH, KW = shape
+    SH = SW = 1
+    OH, OW = Hh - KH + 1, Ww - KW + 1
     x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
     w = (torch.randn(Fo, KH, KW, C, device=DEV) / 6).bfloat16()
     ypre = torch.randn(B, OH, OW, Fo, device=DEV)
