@@ -626,7 +626,11 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                if (row < g.M) {
+                    // GF_WSTORE: this block is the problem's only m-split -> the sole writer
+                    if (g.flags & GF_WSTORE) out[(int64_t)row * g.N + col] = acc[i][j][r];
+                    else atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                }
             }
         }
 }

@@ -20,6 +20,7 @@ enum GemmFlags : int64_t {
     GF_VEC_B = 2,         // B operand chunks are contiguous 8-element vectors
     GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
     GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
+    GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores instead of fp32 atomics
 };
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 

@@ -411,20 +411,45 @@ class HipPopulationEngine(PopulationEngine):
         off = rec["grad"].get(own)
         return None if off is None else mem["grad"].ptr(off)
 
+    def _stream_groups(self, nstreams: int) -> List[List[int]]:
+        """Partition the organisms into <= nstreams groups of similar training FLOPs (LPT)."""
+        P = self.num_organisms
+        k = max(1, min(int(nstreams), P))
+        if k == 1:
+            return [list(range(P))]
+        costs = [float(lay.ir.flops_per_sample()) + 1.0 for lay in self.layouts]
+        order = sorted(range(P), key=lambda o: -costs[o])
+        loads = [0.0] * k
+        groups: List[List[int]] = [[] for _ in range(k)]
+        for o in order:
+            i = min(range(k), key=lambda j: loads[j])
+            groups[i].append(o)
+            loads[i] += costs[o]
+        return [sorted(g) for g in groups if g]
+
     def _build_plan(self, mode: str, B: int, mem, inputs: List[dict], label_ptr: int = 0, target_ptrs=None,
-                    metrics: Optional[torch.Tensor] = None) -> Plan:
-        """mode in {'train', 'infer'}; inputs[org] = {'X': ptr, 'g': ptr} bf16 device pointers."""
+                    metrics: Optional[torch.Tensor] = None, orgs: Optional[Sequence[int]] = None) -> Plan:
+        """mode in {'train', 'infer'}; inputs[org] = {'X': ptr, 'g': ptr} bf16 device pointers.
+        ``orgs``: build the plan for this subset of organisms only (one plan per stream group)."""
         train = mode == "train"
         plan = Plan()
         P = self.num_organisms
+        sel = None if orgs is None else set(int(o) for o in orgs)
+
+        def org_iter():
+            for o_, lay_ in enumerate(self.layouts):
+                if sel is None or o_ in sel:
+                    yield o_, lay_
+
         depth_of = []
         maxd = 0
-        for lay in self.layouts:
+        for o_, lay in enumerate(self.layouts):
             dd = {}
             for n in lay.ir.nodes:
                 dd[n.id] = 0 if n.op == "input" else 1 + max(dd[i] for i in n.inputs)
             depth_of.append(dd)
-            maxd = max(maxd, max(dd.values()))
+            if sel is None or o_ in sel:
+                maxd = max(maxd, max(dd.values()))
 
         def T(arr, dtype=None):
             t = torch.as_tensor(arr, device=self.device) if dtype is None else torch.as_tensor(arr, dtype=dtype,
@@ -532,7 +557,7 @@ class HipPopulationEngine(PopulationEngine):
             bn_rows, bn_cnt = [], []
             c_rows, c_cnt = [], []
             fallbacks = []
-            for o, lay in enumerate(self.layouts):
+            for o, lay in org_iter():
                 ir = lay.ir
                 rec = mem["orgs"][o]
                 for n in ir.nodes:
@@ -626,7 +651,7 @@ class HipPopulationEngine(PopulationEngine):
         # ---- loss ------------------------------------------------------------------------------
         if metrics is not None:
             rows = []
-            for o, lay in enumerate(self.layouts):
+            for o, lay in org_iter():
                 ir = lay.ir
                 rec = mem["orgs"][o]
                 NC, L = ir.num_classes, ir.genotype_size
@@ -634,7 +659,7 @@ class HipPopulationEngine(PopulationEngine):
                                  dlogits=mem["grad"].ptr(rec["grad"][ir.cls_head]) if train else 0,
                                  labels=label_ptr, target=target_ptrs[o], metrics=metrics.data_ptr() + 16 * o,
                                  NC=NC, L=L, B=B, lb=self.lb[o]))
-            plan.loss = (desc_tensor(rows, H.LOSS_DTYPE), P, B)
+            plan.loss = (desc_tensor(rows, H.LOSS_DTYPE), len(rows), B)
         else:
             plan.loss = None
 
@@ -657,7 +682,7 @@ class HipPopulationEngine(PopulationEngine):
 
         if GEMM_IMPL != "v1":
             trows, tcnt = [], []
-            for o, lay in enumerate(self.layouts):
+            for o, lay in org_iter():
                 ir = lay.ir
                 for nid, off in lay.w.items():
                     a = ir.node(nid).attrs
@@ -677,7 +702,7 @@ class HipPopulationEngine(PopulationEngine):
             bn_red, bn_red_cnt = [], []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             fb = []
-            for o, lay in enumerate(self.layouts):
+            for o, lay in org_iter():
                 ir = lay.ir
                 rec = mem["orgs"][o]
                 for n in ir.nodes:
@@ -996,9 +1021,24 @@ class HipPopulationEngine(PopulationEngine):
         self._train_mem = mem
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(P)]
         targets = [gb.data_ptr()] * P
-        plan = self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics)
+        # Organisms are independent: split them into stream groups (LPT on FLOPs) with one plan each,
+        # so the level-by-level launches of different groups overlap on the GPU (fork/join inside the
+        # captured graph).  One group = the single-stream schedule.
+        groups = self._stream_groups(int(os.environ.get("SERANN_STREAMS", "4")))
+        plans = [self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics, orgs=g_) for g_ in groups]
+        if not hasattr(self, "_streams") or len(self._streams) < len(plans):
+            self._streams = [torch.cuda.Stream(device=dev) for _ in plans]
+        streams = self._streams[:len(plans)]
         L = self.lib
         ws = mem["ws"].t
+
+        def run_plan(pl):
+            tmp = Plan()
+            tmp.launches = pl.launches[:pl.fwd_count]
+            tmp.run()
+            self._run_loss(pl, True, B)
+            tmp.launches = pl.launches[pl.fwd_count:]
+            tmp.run()
 
         def step():
             s = H.stream_handle()
@@ -1006,14 +1046,18 @@ class HipPopulationEngine(PopulationEngine):
                            perm_t.data_ptr(), counter.data_ptr(), 0, B, split, xcols, gcols, xb.data_ptr(),
                            gb.data_ptr(), yb.data_ptr(), s)
             L.memset32(ws.data_ptr(), ws.numel(), s)
-            fwd = plan.launches[:plan.fwd_count]
-            bwd = plan.launches[plan.fwd_count:]
-            tmp = Plan()
-            tmp.launches = fwd
-            tmp.run()
-            self._run_loss(plan, True, B)
-            tmp.launches = bwd
-            tmp.run()
+            if len(plans) == 1:
+                run_plan(plans[0])
+            else:
+                main = torch.cuda.current_stream()
+                for st in streams:
+                    st.wait_stream(main)
+                for pl, st in zip(plans, streams):
+                    with torch.cuda.stream(st):
+                        run_plan(pl)
+                for st in streams:
+                    main.wait_stream(st)
+            s = H.stream_handle()
             L.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
                    self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), cfg.lr, cfg.beta1, cfg.beta2,
                    cfg.eps, s)
@@ -1022,7 +1066,8 @@ class HipPopulationEngine(PopulationEngine):
         use_graph = split % B == 0 and steps == split // B
         graph = None
         self.timings["plan_s"] = time.perf_counter() - t_plan
-        self.timings["launches_per_step"] = len(plan.launches) + 5
+        self.timings["launches_per_step"] = sum(len(pl.launches) for pl in plans) + 5
+        self.timings["stream_groups"] = len(plans)
 
         t0 = time.perf_counter()
         train_acc = np.zeros(P)

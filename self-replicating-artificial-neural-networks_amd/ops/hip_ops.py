@@ -26,7 +26,7 @@ COPY_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "rows", "cols", "src_stri
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
-GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32 = 1, 2, 4, 8
+GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE = 1, 2, 4, 8, 16
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -319,7 +319,15 @@ def gemm3_plan(mode: int, rows, dims):
             tiles = np.concatenate(tl).astype(np.int32)
         else:
             bm, bn = gemm3_block(mode, v)
-            tiles = gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn)
+            dms = [dm for _, dm in items]
+            if mode == MODE_WGRAD:
+                tg = [wgrad_target(M, N) for (M, N, K) in dms]
+                tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn)
+                for (r, (M, N, K)), t_ in zip(items, tg):
+                    if wgrad_splits(K, t_, min(32, t_)) == 1:
+                        r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
+            else:
+                tiles = gemm_tiles(dms, mode, bm=bm, bn=bn)
         out.append((v, [r for r, _ in items], tiles))
     return out
 
@@ -330,9 +338,24 @@ def gemm2_block(mode: int, variant: int):
     return (32, variant % 1000) if variant >= 1000 else (128, variant)
 
 
-def gemm_tiles(dims, mode: int, target_ksteps: int = 128, min_ksteps: int = 32, bm: int = BM,
+def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
+    """Number of m-splits (blocks along the reduction) of a WGRAD problem with K reduction rows."""
+    kt = -(-K // BK)
+    if kt <= target_ksteps:
+        return 1
+    return max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps)))
+
+
+def wgrad_target(M: int, N: int) -> int:
+    """k-steps (32 rows) per WGRAD block: small weight matrices split the reduction finer (more
+    parallelism, negligible atomic traffic); large ones keep long blocks (fewer fp32 atomics)."""
+    return 128
+
+
+def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,
                bn: int = BN) -> np.ndarray:
-    """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16)."""
+    """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16).
+    target_ksteps: int, or one value per problem (WGRAD m-split granularity)."""
     rows = []
     for p, (M, N, K) in enumerate(dims):
         tm, tn = -(-M // bm), -(-N // bn)
@@ -340,8 +363,9 @@ def gemm_tiles(dims, mode: int, target_ksteps: int = 128, min_ksteps: int = 32, 
         if tm == 0 or tn == 0:
             continue
         nsplit = 1
-        if mode == MODE_WGRAD and kt > target_ksteps:
-            nsplit = max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps)))
+        tgt = target_ksteps[p] if isinstance(target_ksteps, (list, tuple)) else target_ksteps
+        if mode == MODE_WGRAD:
+            nsplit = wgrad_splits(K, tgt, min(min_ksteps, tgt))
         per = -(-kt // nsplit)
         # k-split outermost, then n, then m: consecutive blocks share the weight (B) panel
         for s in range(nsplit):
