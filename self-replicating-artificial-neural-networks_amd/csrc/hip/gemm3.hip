@@ -1152,8 +1152,191 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
     }
 }
 
+// ==================================================================================================
+// LDS-tiled GEMM for 1x1 / Dense problems (row-major A[M][K] with row stride C, B[N][K]):
+//   FWD   : Y = act(A . B^T + bias)          A = layer input,  B = Wm
+//   DGRAD : dX (+)= (dY * act'(Y)) . B^T     A = dY (+ Y),     B = Wt
+// Block tile 128 x BN (BN = 64 or 128) x 32, 4 waves in a 2 x 2 layout (64 x BN/2 each).  Both
+// operand tiles go through LDS, so the weight tile is fetched once per block instead of once per
+// wave (the direct-fragment kernel re-reads B in every wave), and the next k-step's global loads are in
+// flight while the current step multiplies (register-staged double buffer, one barrier per step).
+// Rows of 40 elements (80 B, an odd number of 16-B slots) keep the 16-row ds_read_b128 fragment reads
+// conflict-free.  The epilogue stages the block's tile in LDS and streams it out with 16-B stores
+// when the block spans all N columns (the usual case: N <= 128).
+template <int MODE, int BN>
+__global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restrict__ descs,
+                                                       const int4* __restrict__ tiles) {
+    constexpr int BM = 128, BK = 32, LDS_ROW = BK + 8;
+    constexpr int NTW = BN / 32;                     // 16-col tiles per wave (2 waves along n)
+    constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = 2 * BN * LDS_ROW;
+    constexpr int STAGE = BM * BN;                   // epilogue staging (bf16 elements)
+    constexpr int LDSN = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
+    __shared__ __attribute__((aligned(16))) bf16_t lds[LDSN];
+    bf16_t* As = lds;                                // [2][BM][LDS_ROW]
+    bf16_t* Bs = lds + ABYTES;                       // [2][BN][LDS_ROW]
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const int M = (int)d.M, N = (int)d.N, K = (int)d.K, act = (int)d.act, flags = (int)d.flags;
+    // A row stride: FWD reads the layer input [M][C] (C == K, or K8 for the shared raw im2col);
+    // DGRAD reads dY [M][F] with F == K for a 1x1 layer
+    const int lda = (MODE == MODE_FWD) ? (int)d.C : K;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    const int m0 = td.y * BM, n0 = td.z * BN;
+    const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
+    const int64_t a_elems = (int64_t)M * lda;
+    const rsrc_t rA = mkrsrc(d.a, a_elems * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? a_elems * 2 : 0);
+    const rsrc_t rB = mkrsrc(d.b, (int64_t)N * K * 2);
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+    const int gact = (MODE == MODE_DGRAD) ? act : ACT_LINEAR;
+
+    // loaders: thread t -> (row t/4 + 64 i, k chunk (t % 4) * 8)
+    const int lr = t >> 2, lk = (t & 3) * 8;
+    constexpr int BPT = BN / 64;                     // B chunks per thread
+    uint4 ra[2], rb[BPT];
+    auto gload = [&](int kt) {
+        const int k = kt * BK + lk;
+        const int run = min(8, K - k);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = m0 + lr + 64 * i;
+            const int off = (m < M && run > 0) ? m * lda + k : -1;
+            uint4 v = bl16(rA, off);
+            if (gact != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), gact);
+            if (run < 8) v = splice(v, zero, run);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BPT; ++i) {
+            const int n = n0 + lr + 64 * i;
+            const int off = (n < N && run > 0) ? n * K + k : -1;
+            uint4 v = bl16(rB, off);
+            if (run < 8) v = splice(v, zero, run);
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lk]) = ra[i];
+#pragma unroll
+        for (int i = 0; i < BPT; ++i)
+            *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
+    };
+
+    f32x4_t acc[4][NTW];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    if (kt0 < kt1) {
+        gload(kt0);
+        sstore(0);
+    }
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const int buf = (kt - kt0) & 1;
+        if (kt + 1 < kt1) gload(kt + 1);
+        Frag fa[4], fb[NTW];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            fa[i].u = *reinterpret_cast<const uint4*>(&As[(buf * BM + wr * 64 + i * 16 + r16) * LDS_ROW + kg]);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+            fb[j].u = *reinterpret_cast<const uint4*>(&Bs[(buf * BN + wc * (BN / 2) + j * 16 + r16) * LDS_ROW + kg]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
+        if (kt + 1 < kt1) sstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue ---------------------------------------------------------------------------------
+    const float* bias = (MODE == MODE_FWD) ? reinterpret_cast<const float*>(d.bias) : nullptr;
+    const int oact = (MODE == MODE_FWD) ? act : ACT_LINEAR;
+    const int rq = (lane >> 4) * 4;
+    if (flags & GF_OUT_F32) {
+        float* o = reinterpret_cast<float*>(d.out);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const int col = n0 + wc * (BN / 2) + j * 16 + r16;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wr * 64 + i * 16 + rq + r;
+                    if (row < M) o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
+                }
+        }
+        return;
+    }
+    bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
+    const bool accum = (flags & GF_ACCUM) != 0;
+    if (n0 == 0 && N <= BN) {
+        // the block's rows [m0, m0 + nrows) x all N columns are one contiguous range of the output
+        bf16_t* st = lds;                            // k loop done (last barrier above)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const int col = wc * (BN / 2) + j * 16 + r16;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st[(wr * 64 + i * 16 + rq + r) * N + col] = f2bf(apply_act(acc[i][j][r] + bv, oact));
+        }
+        __syncthreads();
+        const int nrows = min(BM, M - m0);
+        const int total = nrows * N, nvec = total >> 3;
+        bf16_t* dst = o + (int64_t)m0 * N;           // m0 * N * 2 B is a multiple of 256 B
+        for (int v = t; v < nvec; v += 256) {
+            Frag f;
+            f.u = *reinterpret_cast<const uint4*>(&st[v * 8]);
+            if (accum) {
+                Frag p;
+                p.u = *reinterpret_cast<const uint4*>(&dst[v * 8]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(p.h[e]));
+            }
+            *reinterpret_cast<uint4*>(&dst[v * 8]) = f.u;
+        }
+        for (int e = nvec * 8 + t; e < total; e += 256) {
+            float v = bf2f(st[e]);
+            if (accum) v += bf2f(dst[e]);
+            dst[e] = f2bf(v);
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int col = n0 + wc * (BN / 2) + j * 16 + r16;
+        if (col >= N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + wr * 64 + i * 16 + rq + r;
+                if (row >= M) continue;
+                const int64_t off = (int64_t)row * N + col;
+                float v = apply_act(acc[i][j][r] + bv, oact);
+                if (accum) v += bf2f(o[off]);
+                o[off] = f2bf(v);
+            }
+    }
+}
+
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
-//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4)
+//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4),
+//                 7064 / 7128 for the LDS-tiled 1x1 kernel (BN = 64 / 128; tiles (prob, m tile, n tile, k range))
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
@@ -1218,7 +1401,15 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef C3
         throw std::runtime_error("gemm3: unknown conv variant " + std::to_string(variant));
     }
-    if (mode == MODE_FWD && variant >= 6000) {
+    if (variant == 7064 || variant == 7128) {
+        if (mode == MODE_FWD && variant == 7064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, 64>), grid, block, 0, s, dp, tp);
+        else if (mode == MODE_FWD) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, 128>), grid, block, 0, s, dp, tp);
+        else if (variant == 7064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 64>), grid, block, 0, s, dp, tp);
+        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128>), grid, block, 0, s, dp, tp);
+        SERANN_CHECK(hipGetLastError());
+        return;
+    }
+    if (mode == MODE_FWD && variant >= 6000 && variant < 7000) {
         const int k = variant - 6000;
         if (k == 1) hipLaunchKernelGGL((g3_narrow_fwd_kernel<1>), grid, block, 0, s, dp, tp);
         else if (k == 2) hipLaunchKernelGGL((g3_narrow_fwd_kernel<2>), grid, block, 0, s, dp, tp);

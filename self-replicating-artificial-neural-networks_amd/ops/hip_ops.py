@@ -176,6 +176,8 @@ def gemm3_block(mode: int, variant: int):
     if mode == MODE_WGRAD:
         v = variant % 1000000
         return (v // 1000, v % 1000)
+    if variant in (7064, 7128):
+        return (128, variant - 7000)
     if variant >= 5000:
         return (64 * ((variant // 10) % 10), 16 * (variant % 10))
     nt, rt, kw = variant % 10, (variant // 10) % 10, (variant % 1000) >= 100
@@ -265,6 +267,9 @@ def gemm3_plan(mode: int, rows, dims):
         nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) else None
         if nk is not None:
             v = (6000 if mode == MODE_FWD else 4000000) + nk
+        elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
+              and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
+            v = 7128 if N > 64 else 7064          # LDS-tiled 1x1 / Dense GEMM
         elif mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
             cfg = conv_lds_config(r, N)
             if cfg is not None:
@@ -280,7 +285,7 @@ def gemm3_plan(mode: int, rows, dims):
     out = []
     for v in sorted(groups):
         items = groups[v]
-        if (mode == MODE_FWD and v >= 6000) or (mode == MODE_WGRAD and v >= 4000000):
+        if (mode == MODE_FWD and 6000 <= v < 7000) or (mode == MODE_WGRAD and v >= 4000000):
             per = NARROW_ROWS if mode == MODE_FWD else NARROW_WROWS
             tl = []
             for p, (r, (M, N, K)) in enumerate(items):
