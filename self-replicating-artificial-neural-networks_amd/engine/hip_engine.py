@@ -85,6 +85,8 @@ def device_data(data, device) -> dict:
     """Upload the (shared) training/test arrays once per process, as bf16 / int32."""
     key = (id(data), str(device))
     d = _DEVICE_DATA.get(key)
+    if d is not None and d.get("_src") is not data:
+        d = None          # id() reused by a different object: never serve a stale (wrongly shaped) upload
     if d is None:
         def bf(a):
             return torch.as_tensor(np.ascontiguousarray(a.reshape(len(a), -1)), dtype=torch.float32).to(
@@ -95,6 +97,7 @@ def device_data(data, device) -> dict:
             "train_y": torch.as_tensor(data.train_labels.astype(np.int32), device=device),
             "test_x": bf(data.test_x), "test_g": bf(data.test_g),
             "test_y": torch.as_tensor(data.test_labels.astype(np.int32), device=device),
+            "_src": data,
         }
         _DEVICE_DATA[key] = d
     return d
@@ -665,6 +668,7 @@ class HipPopulationEngine(PopulationEngine):
 
         plan.fwd_count = len(plan.launches)
         if not train:
+            torch.cuda.synchronize(self.device)      # upload fence, as at the end of the train plan
             return plan
 
         # ---- backward --------------------------------------------------------------------------
@@ -844,6 +848,10 @@ class HipPopulationEngine(PopulationEngine):
             for o, n in fb:
                 plan.launches.append(Launch("fn", 0, None, None, 0,
                                             self._fallback_bwd(mem, o, n, inputs, B, target, written)))
+        # descriptor / tile tables are uploaded from pageable host memory: fence them (and any
+        # outstanding work on other streams) before a launch can read them.  Plans are built once per
+        # generation, so this costs nothing on the training hot path.
+        torch.cuda.synchronize(self.device)
         return plan
 
     # ---------------------------------------------------------------------------------------------
@@ -1249,12 +1257,14 @@ class HipPopulationEngine(PopulationEngine):
 
 
 def device_data_for_arrays(x, labels, g, device):
-    key = ("eval", id(x), str(device))
+    key = ("eval", id(x), id(labels), id(g), str(device))
     d = _DEVICE_DATA.get(key)
+    if d is not None and not (d["_src"][0] is x and d["_src"][1] is labels and d["_src"][2] is g):
+        d = None          # ids reused by other arrays: re-upload
     if d is None:
         d = {"x": torch.as_tensor(np.ascontiguousarray(x.reshape(len(x), -1)), dtype=torch.float32).to(device).to(
             torch.bfloat16),
              "g": torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32).to(device).to(torch.bfloat16),
-             "y": torch.as_tensor(labels.astype(np.int32), device=device)}
+             "y": torch.as_tensor(labels.astype(np.int32), device=device), "_src": (x, labels, g)}
         _DEVICE_DATA[key] = d
     return d

@@ -31,6 +31,9 @@ def _desc(rows, dtype):
 
 
 def _run_gemm(mode, rows, dims, impl="v1"):
+    # reference ops (MIOpen / hipBLASLt) may still be in flight, and the descriptor tables below are
+    # uploaded from pageable memory: start every launch from an idle device
+    torch.cuda.synchronize()
     if impl == "v1":
         d = _desc(rows, H.GEMM_DTYPE)
         t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
