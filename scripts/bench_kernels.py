@@ -21,6 +21,48 @@ import numpy as np
 import torch
 
 
+def launch_bytes(la, H):
+    """Minimum HBM bytes a launch must move (each operand read once, output written once) and a short
+    shape list of its problems."""
+    if la.descs is None:
+        return 0.0, []
+    raw = la.descs.cpu().numpy().tobytes()
+    tot, probs = 0.0, []
+    if la.kind in ("gemm", "gemm2", "gemm3"):
+        mode = la.arg[0] if isinstance(la.arg, tuple) else la.arg
+        for r in np.frombuffer(raw, dtype=H.GEMM_DTYPE):
+            M, N, K = int(r["M"]), int(r["N"]), int(r["K"])
+            ob = 4 if int(r["flags"]) & H.GF_OUT_F32 else 2
+            if mode == H.MODE_WGRAD:
+                ohw = max(1, int(r["OH"]) * int(r["OW"]))
+                nb = K // ohw
+                b = K * M * 2 + nb * int(r["H"]) * int(r["W"]) * int(r["C"]) * 2 + M * N * 4
+            elif mode == H.MODE_FWD:
+                ohw = max(1, int(r["OH"]) * int(r["OW"]))
+                nb = M // ohw
+                b = nb * int(r["H"]) * int(r["W"]) * int(r["C"]) * 2 + N * K * 2 + M * N * ob
+            else:
+                b = M * N * 2 + N * K * 2 + M * K * 2 // max(1, int(r["KH"]) * int(r["KW"]))
+            tot += b
+            probs.append((M, N, K, int(r["KH"]), int(r["KW"]), int(r["C"])))
+    elif la.kind == "bn":
+        for r in np.frombuffer(raw, dtype=H.BN_DTYPE):
+            e = int(r["R"]) * int(r["C"])
+            tot += e * 2 * {0: 1, 2: 2, 3: 2, 4: 2, 5: 3}.get(int(la.arg), 2)
+            probs.append((int(r["R"]), int(r["C"])))
+    elif la.kind == "pool":
+        for r in np.frombuffer(raw, dtype=H.POOL_DTYPE):
+            e_in = int(r["B"]) * int(r["H"]) * int(r["W"]) * int(r["C"])
+            e_out = int(r["B"]) * int(r["OH"]) * int(r["OW"]) * int(r["C"])
+            tot += e_in * 2 + e_out * 3
+            probs.append((int(r["B"]), int(r["H"]), int(r["W"]), int(r["C"])))
+    elif la.kind == "copy":
+        for r in np.frombuffer(raw, dtype=H.COPY_DTYPE):
+            tot += int(r["rows"]) * int(r["cols"]) * 4
+            probs.append((int(r["rows"]), int(r["cols"])))
+    return tot, probs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pop", type=int, default=104)
@@ -74,6 +116,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         cls = ""
+        nbytes, probs = launch_bytes(la, H)
         if la.kind in ("gemm", "gemm2", "gemm3"):
             d = np.frombuffer(la.descs.cpu().numpy().tobytes(), dtype=H.GEMM_DTYPE)
             kinds = set()
@@ -89,8 +132,10 @@ def main():
             flops = float(sum(2.0 * r["M"] * r["N"] * r["K"] for r in d))
         else:
             flops = 0.0
-        rows.append(dict(i=i, kind=la.kind, arg=str(la.arg), cls=cls, ms=float(np.median(ts)) * 1e3,
-                         tiles=int(la.n), tflops=flops / max(np.median(ts), 1e-9) / 1e12 if flops else 0.0))
+        med = float(np.median(ts))
+        rows.append(dict(i=i, kind=la.kind, arg=str(la.arg), cls=cls, ms=med * 1e3,
+                         tiles=int(la.n), tflops=flops / max(med, 1e-9) / 1e12 if flops else 0.0,
+                         mbytes=nbytes / 1e6, gbps=nbytes / max(med, 1e-9) / 1e9, probs=probs[:6]))
     agg = defaultdict(lambda: [0.0, 0])
     for r in rows:
         k = (r["kind"], r["arg"], r["cls"])
@@ -101,9 +146,12 @@ def main():
           f"train_flops/step={total_flops / 1e12:.3f} TF -> {total_flops / tot / 1e9:.1f} TF/s")
     for k, (ms, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
         print(f"{k[0]:10s} {k[1]:10s} {k[2]:18s} n={n:4d} {ms:9.3f} ms {100 * ms / tot:5.1f}%")
-    top = sorted(rows, key=lambda r: -r["ms"])[:15]
+    tb = sum(r["mbytes"] for r in rows)
+    print(f"min bytes/step {tb:.1f} MB -> {tb / tot:.1f} GB/s effective over the sum of launches")
+    top = sorted(rows, key=lambda r: -r["ms"])[:40]
     for r in top:
-        print(r)
+        print(f"#{r['i']:3d} {r['kind']:8s} {r['arg']:14s} {r['cls']:16s} {r['ms']:7.3f} ms tiles={r['tiles']:6d} "
+              f"{r['tflops']:6.1f} TF/s {r['mbytes']:8.1f} MB {r['gbps']:7.0f} GB/s {r['probs'][:3]}")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump({"rows": rows, "total_ms": tot, "train_tflop": total_flops / 1e12}, f)

@@ -64,8 +64,13 @@ def build_hip(jobs: int = 4):
              "-Wno-unused-result", f"-I{CSRC / 'hip'}", *_pybind_includes()]
     objs = []
 
+    hdr_mtime = max((h.stat().st_mtime for h in (CSRC / "hip").glob("*.h")), default=0.0)
+
     def compile_one(src):
         obj = build_dir / (src.stem + ".o")
+        # incremental: an object newer than its source and every header is reused
+        if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_mtime):
+            return obj
         _run([hipcc, *flags, "-c", str(src), "-o", str(obj)])
         return obj
 

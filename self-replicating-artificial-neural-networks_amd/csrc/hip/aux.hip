@@ -825,6 +825,33 @@ void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
+// RiboAE encoder input: out[r][e] = table[tokens[r]][e] for r < rows, e < E, where the
+// table already holds the eval-mode BatchNormalization (one channel) folded into the embedding.
+// Token ids are clamped into [0, V) so a corrupt id never reads outside the table.
+__global__ __launch_bounds__(256) void embed_gather_kernel(const int* __restrict__ tokens,
+                                                           const bf16_t* __restrict__ table,
+                                                           bf16_t* __restrict__ out, int64_t rows, int E, int V) {
+    const int64_t total = rows * E;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / E;
+        const int e = (int)(i - r * E);
+        const int tk = min(max(tokens[r], 0), V - 1);
+        out[i] = table[(int64_t)tk * E + e];
+    }
+}
+
+void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t rows, int64_t E, int64_t V,
+                         uint64_t stream) {
+    if (rows <= 0) return;
+    const int64_t total = rows * E;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(embed_gather_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                       as_ptr<const int>(tokens), as_ptr<const bf16_t>(table), as_ptr<bf16_t>(out), rows,
+                       (int)E, (int)V);
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
 // Shared im2col of a single-channel network input (MNIST image X or genotype g) for one
 // (KH, KW, SH, SW) configuration: out[m][k] (row stride K8 = roundup(KH*KW, 8), zero padded).
 // Every organism of the population reads the SAME input batch, so the first-layer convolutions of

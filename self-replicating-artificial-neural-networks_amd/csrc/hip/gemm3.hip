@@ -1262,17 +1262,20 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const int rq = (lane >> 4) * 4;
     if (flags & GF_OUT_F32) {
         float* o = reinterpret_cast<float*>(d.out);
+        const bool split = (MODE == MODE_FWD) && (flags & GF_SPLITK);   // linear activation only
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
             const int col = n0 + wc * (BN / 2) + j * 16 + r16;
             if (col >= N) continue;
-            const float bv = bias ? bias[col] : 0.f;
+            const float bv = (bias && (!split || kt0 == 0)) ? bias[col] : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = m0 + wr * 64 + i * 16 + rq + r;
-                    if (row < M) o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
+                    if (row >= M) continue;
+                    if (split) atomicAdd(o + (int64_t)row * N + col, acc[i][j][r] + bv);
+                    else o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
                 }
         }
         return;

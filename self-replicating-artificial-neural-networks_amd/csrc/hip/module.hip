@@ -43,4 +43,5 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("memset32", &launch_memset32);
     m.def("group_argmax", &launch_group_argmax);
     m.def("imcol", &launch_imcol);
+    m.def("embed_gather", &launch_embed_gather);
 }

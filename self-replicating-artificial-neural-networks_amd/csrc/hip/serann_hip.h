@@ -21,6 +21,8 @@ enum GemmFlags : int64_t {
     GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
     GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
     GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores instead of fp32 atomics
+    GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
+                          // into a zeroed output, the bias added by the split that starts at k = 0
 };
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -47,6 +49,8 @@ void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t s
 void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
 void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t rows, int64_t E, int64_t V,
+                         uint64_t stream);
 void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);
 
 // ---- auxiliary descriptors (int64 fields) ----------------------------------------------------

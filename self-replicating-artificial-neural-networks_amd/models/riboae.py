@@ -14,7 +14,8 @@ generative_net : (100, 2) -> Conv1D(32, 5) -> BN -> Flatten (3,072) -> Dense(350
 * ``DeterministicGAE`` -- softmax codes, loss = -mean log p(x|z) (model.py:107-120).
 
 Inference (``encode_tokens`` / ``decode_tokens``) runs in eval mode; on a GPU the decode path uses
-the HIP kernels (BN folded into the conv/dense weights, grouped MFMA GEMM, fused group-argmax).
+the HIP kernels (BN folded into the conv/dense weights, grouped MFMA GEMM, fused group-argmax), and so
+does the encode path (embedding gather, LDS-halo convolutions, split-K Dense, group-argmax).
 """
 from __future__ import annotations
 
@@ -122,6 +123,7 @@ class GeneticAutoencoder(nn.Module):
         self.generative_net = GenerativeNet(genotype_length, max_phenotype_length, vocabulary_size,
                                             genotype_alphabet_size)
         self._hip_decoder = None
+        self._hip_encoder = None
 
     def decode(self, z_bits: torch.Tensor) -> torch.Tensor:
         logits = self.generative_net(F.one_hot(z_bits.long(), self.alphabet).float())
@@ -139,6 +141,12 @@ class GeneticAutoencoder(nn.Module):
     def encode_tokens(self, tokens: np.ndarray, device="cpu") -> np.ndarray:
         self.eval()
         t = torch.as_tensor(np.asarray(tokens), device=device)
+        if str(device).startswith("cuda"):
+            from ..ops.riboae_ops import HipRiboEncoder, available
+            if available():
+                if self._hip_encoder is None or self._hip_encoder.stale(self):
+                    self._hip_encoder = HipRiboEncoder(self, device)
+                return self._hip_encoder(t).cpu().numpy()
         return self.encode(t).cpu().numpy()
 
     @torch.no_grad()

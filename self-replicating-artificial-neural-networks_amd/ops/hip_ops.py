@@ -26,7 +26,7 @@ COPY_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "rows", "cols", "src_stri
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
-GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE = 1, 2, 4, 8, 16
+GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK = 1, 2, 4, 8, 16, 32
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -354,7 +354,10 @@ def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
 def wgrad_target(M: int, N: int) -> int:
     """k-steps (32 rows) per WGRAD block: small weight matrices split the reduction finer (more
     parallelism, negligible atomic traffic); large ones keep long blocks (fewer fp32 atomics)."""
-    return 128
+    return _WGRAD_TARGET
+
+
+_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128")) if "_os" in globals() else 128
 
 
 def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,

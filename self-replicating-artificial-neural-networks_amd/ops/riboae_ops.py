@@ -1,9 +1,15 @@
-"""HIP decode path of the ribosomal autoencoder (K33-K35): genotype bits -> token ids.
+"""HIP inference paths of the ribosomal autoencoder (reference ribosomal_autoencoder/model.py:17-52,
+evolutionary_experiment/logic/ribosomal_autoencoder.py:116-124).
 
-Eval-mode BatchNormalization layers are folded into the preceding Conv1D / Dense weights, so decode
-is two grouped MFMA GEMM launches (Conv1D 2->32 k5 as an implicit-GEMM conv; Dense 3072 -> 350*V
-with fp32 output) and one fused group-argmax launch.  log_softmax is monotone, so it is never
-materialised (inference never materialises log-probs).
+* Decode (K33-K35): genotype bits -> token ids.  Eval-mode BatchNormalization layers are folded into
+  the preceding Conv1D / Dense weights, so decode is two grouped MFMA GEMM launches (Conv1D 2->32 k5 as
+  an implicit-GEMM conv; Dense 3072 -> 350*V with fp32 output) and one fused group-argmax launch.
+  log_softmax is monotone, so it is never materialised.
+* Encode (K30-K32, K35): token ids -> genotype bits.  The one-channel BatchNormalization after the
+  embedding is folded into the embedding table, the BatchNormalizations after the three Conv2Ds into
+  their weights and biases.  Encode is an embedding-gather launch, three LDS-halo MFMA convolutions
+  (350x50x1 -> 346x46x32 -> 344x44x16 -> 342x42x16, NHWC bf16), the split-K LDS-tiled Dense
+  229,824 -> 200 (fp32 atomics, K >> M, N) and a group-argmax over the alphabet.
 """
 from __future__ import annotations
 
@@ -78,3 +84,121 @@ class HipRiboDecoder:
         lib.grouped_gemm(H.MODE_FWD, d2.data_ptr(), t2.data_ptr(), len(t2), s)
         lib.group_argmax(logits.data_ptr(), out.data_ptr(), B * L, V, s)
         return out.long()
+
+
+def _fold_bn(bn):
+    s_ = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    return s_, bn.bias - bn.running_mean * s_
+
+
+class HipRiboEncoder:
+    """Eval-mode ``inference_net`` + argmax on the HIP kernels (see the module docstring)."""
+
+    SPLIT_KSTEPS = 48           # 32-wide k steps per split-K block of the flatten Dense
+
+    def __init__(self, model, device, chunk: int = 128):
+        self.device = torch.device(device)
+        self.version = getattr(model, "_param_version", 0)
+        self.model_id = id(model)
+        self.chunk = int(chunk)
+        net = model.inference_net
+        self.L, self.E = net.max_len, net.emb_dim
+        self.G, self.A = net.genotype_length, net.alphabet
+        with torch.no_grad():
+            s0, t0 = _fold_bn(net.bn0)
+            table = net.embedding.weight * s0[0] + t0[0]                    # (V, E)
+            self.V = table.shape[0]
+            self.table = table.to(self.device, torch.bfloat16).contiguous()
+            self.convs = []
+            for conv, bn in ((net.conv1, net.bn1), (net.conv2, net.bn2), (net.conv3, net.bn3)):
+                sc, sh = _fold_bn(bn)
+                w = (conv.weight * sc[:, None, None, None]).permute(0, 2, 3, 1).contiguous()  # [F][KH][KW][C]
+                b = conv.bias * sc + sh
+                self.convs.append((w.to(self.device, torch.bfloat16).contiguous(),
+                                   b.to(self.device, torch.float32).contiguous(), conv.kernel_size))
+            self.wd = net.dense.weight.to(self.device, torch.bfloat16).contiguous()          # [N][K]
+            self.bd = net.dense.bias.to(self.device, torch.float32).contiguous()
+        self._plans = {}
+
+    def stale(self, model) -> bool:
+        return id(model) != self.model_id or getattr(model, "_param_version", 0) != self.version
+
+    def _plan(self, B: int):
+        """Buffers, descriptors and tile tables for a chunk of B sequences (cached per B)."""
+        if B in self._plans:
+            return self._plans[B]
+        dev = self.device
+        Hh, Ww, C = self.L, self.E, 1
+        x = torch.empty(B, Hh, Ww, C, dtype=torch.bfloat16, device=dev)
+        bufs, launches = [x], []
+        cur = x
+        for w, b, (kh, kw) in self.convs:
+            F = w.shape[0]
+            OH, OW = Hh - kh + 1, Ww - kw + 1
+            y = torch.empty(B, OH, OW, F, dtype=torch.bfloat16, device=dev)
+            K = kh * kw * C
+            row = dict(a=cur.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=Hh, W=Ww, C=C,
+                       OH=OH, OW=OW, F=F, KH=kh, KW=kw, SH=1, SW=1, M=B * OH * OW, N=F, K=K, act=0,
+                       flags=(H.GF_VEC_B if C % 8 == 0 else 0) | (H.GF_VEC_A if C % 8 == 0 else 0))
+            for v, rws, tiles in H.gemm3_plan(H.MODE_FWD, [row], [(B * OH * OW, F, K)]):
+                d = torch.as_tensor(np.frombuffer(H.gemm_desc_array(rws).tobytes(), dtype=np.uint8).copy(),
+                                    device=dev)
+                t = torch.as_tensor(np.ascontiguousarray(tiles), device=dev)
+                launches.append((v, d, t))
+            bufs.append(y)
+            cur, Hh, Ww, C = y, OH, OW, F
+        K = Hh * Ww * C
+        N = self.G * self.A
+        logits = torch.zeros(B, N, dtype=torch.float32, device=dev)
+        row = dict(a=cur.data_ptr(), b=self.wd.data_ptr(), out=logits.data_ptr(), bias=self.bd.data_ptr(),
+                   H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=B, N=N, K=K, act=0,
+                   flags=H.GF_OUT_F32 | H.GF_SPLITK | (H.GF_VEC_A | H.GF_VEC_B if K % 8 == 0 else 0))
+        d = torch.as_tensor(np.frombuffer(H.gemm_desc_array([row]).tobytes(), dtype=np.uint8).copy(), device=dev)
+        kt = -(-K // H.BK)
+        per = self.SPLIT_KSTEPS
+        tl = []
+        for k0 in range(0, kt, per):
+            packed = k0 | (min(kt, k0 + per) << 16)
+            for tm in range(-(-B // 128)):
+                for tn in range(-(-N // 128)):
+                    tl.append((0, tm, tn, packed))
+        t = torch.as_tensor(np.asarray(tl, dtype=np.int32), device=dev)
+        dense = (7128, d, t)
+        bits = torch.empty(B * self.G, dtype=torch.int32, device=dev)
+        plan = dict(x=x, bufs=bufs, convs=launches, dense=dense, logits=logits, bits=bits)
+        self._plans[B] = plan
+        return plan
+
+    @torch.no_grad()
+    def logits(self, tokens: torch.Tensor) -> torch.Tensor:
+        """(n, L) token ids -> (n, G, A) fp32 logits of the eval-mode inference net."""
+        return self._run(tokens, want_logits=True)
+
+    @torch.no_grad()
+    def __call__(self, tokens: torch.Tensor) -> torch.Tensor:
+        return self._run(tokens, want_logits=False)
+
+    def _run(self, tokens: torch.Tensor, want_logits: bool):
+        tok = tokens.to(self.device).to(torch.int32)
+        n = tok.shape[0]
+        if tok.shape[1] != self.L:
+            raise ValueError(f"token sequences must have length {self.L}, got {tok.shape[1]}")
+        lib, s = H.lib(), H.stream_handle()
+        outs = []
+        for c0 in range(0, n, self.chunk):
+            part = tok[c0:c0 + self.chunk].contiguous()
+            B = part.shape[0]
+            pl = self._plan(B)
+            lib.embed_gather(part.data_ptr(), self.table.data_ptr(), pl["x"].data_ptr(), B * self.L, self.E,
+                             self.V, s)
+            for v, d, t in pl["convs"]:
+                lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
+            pl["logits"].zero_()
+            v, d, t = pl["dense"]
+            lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
+            if want_logits:
+                outs.append(pl["logits"].view(B, self.G, self.A).clone())
+            else:
+                lib.group_argmax(pl["logits"].data_ptr(), pl["bits"].data_ptr(), B * self.G, self.A, s)
+                outs.append(pl["bits"].view(B, self.G).long().clone())
+        return torch.cat(outs, 0)

@@ -107,7 +107,7 @@ def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out
         loss = float(metrics["loss"].detach())
         history.append(loss)
         if b % log_every == 0:
-            log(f'Batch: {b} | Loss: {loss:.5f} | NLL: {float(metrics["nll"]):.5f} | KL: {float(metrics["kld"]):.5f} '
+            log(f'Batch: {b} | Loss: {loss:.5f} | NLL: {float(metrics["nll"].detach()):.5f} | KL: {float(metrics["kld"].detach()):.5f} '
                 f'| {(time.perf_counter() - t0) / log_every * 1e3:.1f} ms/batch')
             t0 = time.perf_counter()
         if vocabulary is not None and demo_every and b % demo_every == 0:
