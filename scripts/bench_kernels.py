@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--out", default="gpurun_out/bench_kernels.json")
+    ap.add_argument("--only", type=str, default="", help="comma-separated launch indices to time (profiling)")
     a = ap.parse_args()
     from serann.engine.hip_engine import HipPopulationEngine, Plan
     from serann.genome.codec import decoded_form
@@ -105,7 +106,10 @@ def main():
     total_flops = 0.0
     for ir in irs:
         total_flops += 3 * ir.flops_per_sample() * B
+    only = {int(v) for v in a.only.split(",") if v.strip()}
     for i, la in enumerate(plan.launches):
+        if only and i not in only:
+            continue
         one = Plan()
         one.launches = [la]
         ts = []

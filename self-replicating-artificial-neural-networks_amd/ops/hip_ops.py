@@ -348,7 +348,7 @@ def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
     kt = -(-K // BK)
     if kt <= target_ksteps:
         return 1
-    return max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps)))
+    return max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps), _WGRAD_MAXSPLIT))
 
 
 def wgrad_target(M: int, N: int) -> int:
@@ -357,7 +357,8 @@ def wgrad_target(M: int, N: int) -> int:
     return _WGRAD_TARGET
 
 
-_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128")) if "_os" in globals() else 128
+_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+_WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
 def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,
