@@ -825,6 +825,37 @@ void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
+// Split-K finalize of the LDS-tiled FWD GEMM (GF_SPLITWS): out[m][n] = bf16(act(sum_s ws[s][m][n] +
+// bias[n])).  Grouped: tiles (problem, chunk of SPLITFIN_ELEMS outputs).
+constexpr int SPLITFIN_ELEMS = 2048;
+
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(const SplitFinDesc* __restrict__ descs,
+                                                              const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const SplitFinDesc& d = descs[td.x];
+    const int64_t MN = d.M * d.N;
+    const int N = (int)d.N, S = (int)d.S, act = (int)d.act;
+    const float* __restrict__ ws = reinterpret_cast<const float*>(d.ws);
+    const float* __restrict__ bias = reinterpret_cast<const float*>(d.bias);
+    bf16_t* __restrict__ out = reinterpret_cast<bf16_t*>(d.out);
+    const int64_t e0 = (int64_t)td.y * SPLITFIN_ELEMS;
+    const int64_t e1 = min(MN, e0 + SPLITFIN_ELEMS);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        float v = 0.f;
+        for (int s_ = 0; s_ < S; ++s_) v += ws[s_ * MN + e];
+        if (bias) v += bias[(int)(e % N)];
+        out[e] = f2bf(apply_act(v, act));
+    }
+}
+
+void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
+                       as_ptr<const SplitFinDesc>(descs), as_ptr<const int2>(tiles));
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
 // RiboAE encoder input: out[r][e] = table[tokens[r]][e] for r < rows, e < E, where the
 // table already holds the eval-mode BatchNormalization (one channel) folded into the embedding.
 // Token ids are clamped into [0, V) so a corrupt id never reads outside the table.

@@ -1303,6 +1303,23 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const float* bias = (MODE == MODE_FWD) ? reinterpret_cast<const float*>(d.bias) : nullptr;
     const int oact = (MODE == MODE_FWD) ? act : ACT_LINEAR;
     const int rq = (lane >> 4) * 4;
+    if (MODE == MODE_FWD && (flags & GF_SPLITWS)) {
+        // raw fp32 partial of this k split; splitk_finalize adds the splits, bias and activation
+        float* w = reinterpret_cast<float*>(d.aux) + (int64_t)(kt0 / (int)d.kper) * M * N;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+            const int col = n0 + wc * (BN / 2) + j * 16 + r16;
+            if (col >= N) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wr * 64 + i * 16 + rq + r;
+                    if (row < M) w[(int64_t)row * N + col] = acc[i][j][r];
+                }
+        }
+        return;
+    }
     if (flags & GF_OUT_F32) {
         float* o = reinterpret_cast<float*>(d.out);
         const bool split = (MODE == MODE_FWD) && (flags & GF_SPLITK);   // linear activation only

@@ -17,6 +17,7 @@ static py::dict desc_sizes() {
     d["LossDesc"] = sizeof(LossDesc);
     d["TransDesc"] = 5 * sizeof(int64_t);
     d["ImcolDesc"] = sizeof(ImcolDesc);
+    d["SplitFinDesc"] = sizeof(SplitFinDesc);
     return d;
 }
 
@@ -44,4 +45,5 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("group_argmax", &launch_group_argmax);
     m.def("imcol", &launch_imcol);
     m.def("embed_gather", &launch_embed_gather);
+    m.def("splitk_finalize", &launch_splitk_finalize);
 }

@@ -14,6 +14,7 @@ struct GemmDesc {
     // divisors the v3 kernels need: q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31.
     int64_t dvC, dvKW, dvOW, dvOHW, dvF, dvW, dvHW, dvSH, dvSW;
     int64_t dvCp;     // magic of Cp = C rounded up to 8 (LDS-halo conv kernels)
+    int64_t kper;     // GF_SPLITWS: k steps (32) per split; split s writes aux + s * M * N (fp32)
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
@@ -21,6 +22,9 @@ enum GemmFlags : int64_t {
     GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
     GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
     GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores instead of fp32 atomics
+    GF_SPLITWS = 64,      // FWD (LDS-tiled kernel): k range split over blocks; each split stores its raw
+                          // fp32 partial tile to the workspace aux[split][M][N]; splitk_finalize sums
+                          // the splits and applies bias + activation (no atomics, no zeroing)
     GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
                           // into a zeroed output, the bias added by the split that starts at k = 0
 };
@@ -49,6 +53,7 @@ void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t s
 void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
 void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t rows, int64_t E, int64_t V,
                          uint64_t stream);
 void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);
@@ -62,6 +67,7 @@ struct BnDesc {
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
 struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
+struct SplitFinDesc { int64_t ws, out, bias, M, N, S, act, flags; };      // flags: reserved
 struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;

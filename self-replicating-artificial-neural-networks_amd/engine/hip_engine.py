@@ -157,6 +157,8 @@ class Plan:
                 L.pool(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "copy":
                 L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "splitfin":
+                L.splitk_finalize(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "fn":
                 la.fn()
             else:
@@ -482,10 +484,25 @@ class HipPopulationEngine(PopulationEngine):
                 return
             if GEMM_IMPL == "v3":
                 clean = [{k: val for k, val in r.items() if k != "b_v1"} for r in rows]
-                for v, rws, tiles in H.gemm3_plan(mode_, clean, dims):
-                    if len(tiles):
-                        plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
-                                                    len(tiles)))
+                for v, rws, tiles in H.gemm3_plan(mode_, clean, dims, splitk=True):
+                    if not len(tiles):
+                        continue
+                    # split-K FWD problems (merged Dense): fp32 partials per split in a workspace of
+                    # the plan, then one grouped finalize launch (sum of splits + bias + activation)
+                    fin = []
+                    for r in rws:
+                        ns = int(r.pop("_split", 1))
+                        if ns > 1:
+                            wsb = torch.empty(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
+                            plan.keep.append(wsb)
+                            r["aux"] = wsb.data_ptr()
+                            fin.append(dict(ws=r["aux"], out=r["out"], bias=r.get("bias", 0), M=r["M"], N=r["N"],
+                                            S=ns, act=r.get("act", 0)))
+                    plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
+                                                len(tiles)))
+                    if fin:
+                        add_chunked("splitfin", 0, fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in fin],
+                                    H.SPLITFIN_ELEMS)
                 return
             groups = {}
             for r, dm in zip(rows, dims):

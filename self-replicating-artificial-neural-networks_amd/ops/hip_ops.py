@@ -14,7 +14,8 @@ _I = np.int64
 GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "KH", "KW", "SH", "SW",
                "M", "N", "K", "act", "flags",
                # fast-division magics for the v3 kernels (filled by fill_gemm_divisors)
-               "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW", "dvCp"]
+               "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW", "dvCp",
+               "kper"]      # GF_SPLITWS: k steps per split
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 ACTBWD_DTYPE = np.dtype([(f, _I) for f in ["dy", "y", "dz", "dbias", "M", "N", "act", "flags"]])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
@@ -23,10 +24,12 @@ BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "m
 POOL_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "idx", "dy", "dx", "B", "H", "W", "C", "OH", "OW", "PH", "PW",
                                          "SH", "SW", "flags"]])
 COPY_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "rows", "cols", "src_stride", "dst_stride", "flags"]])
+SPLITFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "bias", "M", "N", "S", "act", "flags"]])
+SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kernel
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
-GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK = 1, 2, 4, 8, 16, 32
+GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS = 1, 2, 4, 8, 16, 32, 64
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -112,7 +115,7 @@ def check_layouts():
     sizes = lib().desc_sizes()
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
-                     ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE)]:
+                     ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
@@ -254,12 +257,15 @@ def narrow_k(geo: dict, mode: int, M: int, N: int, K: int):
     return None
 
 
-def gemm3_plan(mode: int, rows, dims):
+def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     """Group the problems of one grouped launch by v3 kernel instantiation.
 
     Returns [(variant, rows, tiles int32 (n, 4))].  FWD convolutions whose input patch fits in LDS go
     to the halo kernel (tiles (prob, image, first pixel, column tile)); everything else to the
-    direct / WGRAD kernels (tiles (prob, m tile, n tile, k range))."""
+    direct / WGRAD kernels (tiles (prob, m tile, n tile, k range)).
+    ``splitk``: LDS-tiled FWD problems with few output tiles and a long reduction get k splits (rows
+    marked ``_split`` = number of splits, plus GF_SPLITWS and kper); the caller provides the fp32
+    workspace (``aux``) and runs splitk_finalize after the launch."""
     groups = {}
     for r, dm in zip(rows, dims):
         M, N, K = dm
@@ -270,6 +276,10 @@ def gemm3_plan(mode: int, rows, dims):
         elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
               and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
             v = 7128 if N > 64 else 7064          # LDS-tiled 1x1 / Dense GEMM
+            if mode == MODE_FWD and splitk:
+                ns = tiled_fwd_splits(M, N, K, v - 7000, int(r.get("flags", 0)))
+                if ns > 1:
+                    r["_split"] = ns
         elif mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
             cfg = conv_lds_config(r, N)
             if cfg is not None:
@@ -331,10 +341,46 @@ def gemm3_plan(mode: int, rows, dims):
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
+            elif mode == MODE_FWD and v in (7064, 7128):
+                tl = []
+                for p, (r, (M, N, K)) in enumerate(items):
+                    kt = -(-K // BK)
+                    ns = int(r.get("_split", 1))
+                    per = -(-kt // ns)
+                    if ns > 1:
+                        r["kper"] = per
+                        r["flags"] = int(r.get("flags", 0)) | GF_SPLITWS
+                    t = gemm_tiles([(M, N, K)], mode, bm=bm, bn=bn)
+                    for s_ in range(ns):
+                        k0, k1 = s_ * per, min(kt, (s_ + 1) * per)
+                        if k0 >= k1:
+                            continue
+                        ts = t.copy()
+                        ts[:, 0] = p
+                        ts[:, 3] = k0 | (k1 << 16)
+                        tl.append(ts)
+                tiles = np.concatenate(tl).astype(np.int32) if tl else np.zeros((0, 4), np.int32)
             else:
                 tiles = gemm_tiles(dms, mode, bm=bm, bn=bn)
         out.append((v, [r for r, _ in items], tiles))
     return out
+
+
+SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "48"))   # target k steps per split (0: off)
+
+
+def tiled_fwd_splits(M: int, N: int, K: int, bn: int, flags: int) -> int:
+    """k splits of an LDS-tiled FWD problem.  Merged-Dense layers have few output tiles (M = batch
+    rows, N <= 256) and a long reduction (K up to ~20k): unsplit, a handful of blocks each walk hundreds
+    of latency-bound k steps.  Split so every block walks about SPLIT_KSTEPS k steps (at most 16
+    splits); bf16 problems only (GF_OUT_F32 / GF_ACCUM outputs are never split)."""
+    if SPLIT_KSTEPS <= 0 or flags & (GF_OUT_F32 | GF_ACCUM | GF_SPLITK):
+        return 1
+    kt = -(-K // BK)
+    tiles = -(-M // 128) * -(-N // bn)
+    if tiles >= 256 or kt < 2 * SPLIT_KSTEPS:
+        return 1
+    return int(min(16, kt // SPLIT_KSTEPS))
 
 
 def gemm2_block(mode: int, variant: int):

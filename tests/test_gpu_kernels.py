@@ -121,6 +121,50 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     assert _rel(dw, ref_dw) < 2e-5
 
 
+def test_tiled_fwd_split_k_with_finalize():
+    """Merged-Dense FWD with a long reduction: k split over blocks (fp32 partials in a workspace),
+    then the grouped finalize (sum of splits + bias + activation) -- the engine's GF_SPLITWS path."""
+    torch.cuda.synchronize()
+    probs = [(750, 148, 12444, "relu"), (750, 110, 3776, "sigmoid"), (300, 40, 5000, "linear"), (750, 110, 130, "relu")]
+    rows, dims, refs, outs, keep = [], [], [], [], []
+    for M, N, K, act in probs:
+        x = torch.randn(M, K, device=DEV).bfloat16()
+        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+        b = torch.randn(N, device=DEV)
+        y = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        keep += [x, w, b, y]
+        rows.append(dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=1, W=1, C=K, OH=1, OW=1,
+                         F=N, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=K, act=H.ACT_CODES[act],
+                         flags=H.GF_VEC_A | H.GF_VEC_B if K % 8 == 0 else 0))
+        dims.append((M, N, K))
+        r = x.float() @ w.float().t() + b
+        refs.append({"relu": torch.relu, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](r))
+        outs.append(y)
+    plans = H.gemm3_plan(H.MODE_FWD, rows, dims, splitk=True)
+    nsplit = 0
+    for v, rws, tiles in plans:
+        fin = []
+        for r in rws:
+            ns = int(r.pop("_split", 1))
+            if ns > 1:
+                nsplit += 1
+                wsb = torch.full((ns * r["M"] * r["N"],), float("nan"), device=DEV)   # every slot is written
+                keep.append(wsb)
+                r["aux"] = wsb.data_ptr()
+                fin.append(dict(ws=r["aux"], out=r["out"], bias=r["bias"], M=r["M"], N=r["N"], S=ns, act=r["act"]))
+        d = _desc(rws, H.GEMM_DTYPE)
+        t = torch.as_tensor(tiles, device=DEV)
+        H.lib().gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+        if fin:
+            fd = _desc(fin, H.SPLITFIN_DTYPE)
+            ft = torch.as_tensor(H.chunk_tiles([f["M"] * f["N"] for f in fin], H.SPLITFIN_ELEMS), device=DEV)
+            H.lib().splitk_finalize(fd.data_ptr(), ft.data_ptr(), len(ft), H.stream_handle())
+    torch.cuda.synchronize()
+    assert nsplit == 3
+    for y, r in zip(outs, refs):
+        assert _rel(y.float(), r) < 6e-3
+
+
 def test_transpose_weights_kernel():
     w = torch.randn(37, 3, 5, 13, device=DEV).bfloat16()
     out = torch.zeros(13, 3, 5, 37, dtype=torch.bfloat16, device=DEV)
