@@ -1,16 +1,19 @@
 #!/bin/bash
-# kernel numerics + per-launch timing + bench for the default path and one A/B variant ($1 = SERANN_GEMM3_OFF list)
+# A/B of the current in-tree kernels against ab/prev (built by scripts/ab_build.sh): interleaved
+# step-time runs, then per-launch timings of both.
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_engine.py -q -x > gpurun_out/kt.log 2>&1 || { tail -25 gpurun_out/kt.log; exit 1; }
-tail -1 gpurun_out/kt.log
-timeout -k 10 300 python scripts/bench_kernels.py --out gpurun_out/bk3.json > gpurun_out/bk3.log 2>&1 || { tail -5 gpurun_out/bk3.log; exit 1; }
-head -2 gpurun_out/bk3.log | tail -1
-timeout -k 10 400 python bench.py --steps 2 --warmup 1 > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
-echo "default:"; tail -1 gpurun_out/bench.log | cut -c1-300
-if [ -n "$1" ]; then
-  SERANN_GEMM3_OFF=$1 timeout -k 10 300 python scripts/bench_kernels.py --out gpurun_out/bk3_off.json > gpurun_out/bk3_off.log 2>&1 || exit 1
-  head -2 gpurun_out/bk3_off.log | tail -1
-  SERANN_GEMM3_OFF=$1 timeout -k 10 400 python bench.py --steps 2 --warmup 1 > gpurun_out/bench_off.log 2>&1 || exit 1
-  echo "off=$1:"; tail -1 gpurun_out/bench_off.log | cut -c1-300
+for i in 1 2; do
+  for v in new prev; do
+    if [ $v = prev ]; then export SERANN_NATIVE_DIR=$PWD/ab/prev; else unset SERANN_NATIVE_DIR; fi
+    timeout -k 10 200 python scripts/bench_step.py --streams ${STREAMS:-4,1} > gpurun_out/ab_$v$i.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ab_$v$i.log; exit 1; }
+    grep streams= gpurun_out/ab_$v$i.log | sed "s/^/$v$i /"
+  done
+done
+if [ -n "$KB" ]; then
+  for v in new prev; do
+    if [ $v = prev ]; then export SERANN_NATIVE_DIR=$PWD/ab/prev; else unset SERANN_NATIVE_DIR; fi
+    timeout -k 10 200 python scripts/bench_kernels.py --pop 125 --out gpurun_out/kb_$v.json > gpurun_out/kb_$v.log 2>&1 || { echo "kb $v failed"; exit 1; }
+    sed -n 2p gpurun_out/kb_$v.log
+  done
 fi

@@ -17,7 +17,8 @@ def load(name: str, required: bool = False):
     if name in _cache:
         return _cache[name]
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    path = NATIVE_DIR / f"{name}{suffix}"
+    # SERANN_NATIVE_DIR: load the extensions of another in-tree build (A/B timing of two kernel versions)
+    path = Path(os.environ.get("SERANN_NATIVE_DIR") or NATIVE_DIR) / f"{name}{suffix}"
     mod = None
     if path.exists():
         if name.startswith("serann_hip"):
