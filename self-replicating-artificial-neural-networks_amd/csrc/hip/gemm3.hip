@@ -717,26 +717,11 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     // ---- stage the patch: input rows [oh_a*SH, oh_a*SH + rows_in) of image b ----------------------
     const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * g.H * g.W * g.C * 2);
     const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
-    // 16-B pieces u = (pixel, 8 channels), four per thread in flight per batch (the loads of a batch
-    // are all issued before its LDS writes)
-    {
-        const int C8 = Cp >> 3;
-        const int npieces = npix * C8;
-        for (int u0 = 0; u0 < npieces; u0 += 4 * 256) {
-            uint4 v[4];
-            int dst[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int u = u0 + k * 256 + t;
-                const int p = fdiv(u * 8, dCp);
-                const int c = u * 8 - p * Cp;
-                dst[k] = u < npieces ? p * Cs + c : -1;
-                v[k] = bl16(rA, u < npieces ? gbase + p * g.C + c : -1);
-                if (g.C & 7) v[k] = splice(v[k], zero, g.C - c);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (dst[k] >= 0) *reinterpret_cast<uint4*>(&patch[dst[k]]) = v[k];
+    for (int p = t; p < npix; p += 256) {
+        for (int c = 0; c < Cp; c += 8) {
+            uint4 v = bl16(rA, gbase + p * g.C + c);
+            if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+            *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
         }
     }
 
@@ -852,7 +837,8 @@ template <int BMF, int BNK, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
     constexpr int TM = 128, LDA = BMF + 8;
-    __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH];
+    // patch + one 16-B dump slot for the staging writes of pieces past the chunk's patch
+    __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH + 8];
     __shared__ __attribute__((aligned(16))) bf16_t As[TM * LDA];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
@@ -917,21 +903,6 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     constexpr int ALD = (TM * ACH + 255) / 256;     // 16-B dZ pieces per thread
     uint4 pre[PLD], apre[ALD];
     int cur_npix = 0;
-    // piece k of this thread (16 B = 8 padded channels) is pixel p(k), channel c(k) of the patch.  When
-    // the pieces per pixel C8 divide 256 (power-of-two channel counts: every conv output feeding a
-    // conv) c(k) is constant and p(k) = p(0) + k * 256 / C8 -- no per-piece division.
-    const bool lin = (256 % C8) == 0;
-    const int p0 = fdiv(t * 8, dCp), c0 = t * 8 - p0 * Cp, pstep = lin ? 256 / C8 : 0;
-    auto piece = [&](int k, int& p, int& c) {
-        if (lin) {
-            p = p0 + k * pstep;
-            c = c0;
-        } else {
-            const int u = t + k * 256;
-            p = fdiv(u * 8, dCp);
-            c = u * 8 - p * Cp;
-        }
-    };
     auto fetch = [&](int ch) {
         const int b = ch / tpi;
         const int m0 = (ch - b * tpi) * TM;
@@ -943,11 +914,19 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         cur_npix = npix;
 #pragma unroll
         for (int k = 0; k < PLD; ++k) {
-            int p, c;
-            piece(k, p, c);
-            uint4 v = bl16(rX, p < npix ? gbase + p * g.C + c : -1);
-            if (g.C & 7) v = splice(v, zero, g.C - c);          // zero the pad channels (not in K)
-            pre[k] = v;
+            const int u = t + k * 256;
+            const int p = fdiv(u * 8, dCp);
+            const int c = u * 8 - p * Cp;
+            pre[k] = bl16(rX, p < npix ? gbase + p * g.C + c : -1);
+        }
+        if (g.C & 7) {                                 // zero the pad channels (not in the K range)
+#pragma unroll
+            for (int k = 0; k < PLD; ++k) {
+                const int u = t + k * 256;
+                const int p = fdiv(u * 8, dCp);
+                const int c = u * 8 - p * Cp;
+                pre[k] = splice(pre[k], zero, g.C - c);
+            }
         }
 #pragma unroll
         for (int k = 0; k < ALD; ++k) {
@@ -972,11 +951,10 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         __syncthreads();                              // previous chunk's LDS reads are done
 #pragma unroll
         for (int k = 0; k < PLD; ++k) {
-            int p, c;
-            piece(k, p, c);
-            // pieces past the chunk's patch are skipped (exec-masked), not sent to a shared dump slot:
-            // 64 lanes writing one LDS address serialise
-            if (p < npix) *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = pre[k];
+            const int u = t + k * 256;
+            const int p = fdiv(u * 8, dCp);
+            const int c = u * 8 - p * Cp;
+            *reinterpret_cast<uint4*>(&patch[p < npix ? p * Cs + c : PATCH]) = pre[k];
         }
 #pragma unroll
         for (int k = 0; k < ALD; ++k) {
