@@ -2,8 +2,8 @@
 """BASELINE config #3: ribosomal-autoencoder training (bf16 autocast) on one MI355X, synthetic dataset.
 
 Reports training batches/s and sequences/s (batch 512, ConcreteGAE, schedules of training.py), plus
-the HIP decode path throughput (genotypes decoded per second; BN folded, grouped MFMA GEMM + fused
-group-argmax) and its agreement with the torch eval-mode decode.
+the HIP decode / encode path throughput (genotypes decoded and sequences encoded per second; BN folded,
+grouped MFMA GEMMs + fused group-argmax) and their agreement with the torch eval-mode model.
 """
 from __future__ import annotations
 
@@ -62,6 +62,37 @@ def main():
         torch.cuda.synchronize()
     out["decode_genotypes_per_sec"] = a.decode_n / (time.perf_counter() - t0)
     out["decode_token_agreement_vs_torch"] = float((got == ref).mean())
+    # encode (K30-K32, K35): token sequences -> genotype bits on the HIP path
+    toks = seqs[np.random.default_rng(1).integers(0, len(seqs), a.decode_n)]
+    # torch reference in chunks of 512: on this ROCm image the fp32 inference net on one 4096-sequence
+    # batch (conv activations > 4 GB) returns wrong logits (measured: 48 % agreement with the same
+    # model on 512-sequence chunks), so the whole-batch call cannot serve as the reference
+    with torch.no_grad():
+        ref_bits = np.concatenate([model.encode(torch.as_tensor(toks[i:i + 512], device=dev)).cpu().numpy()
+                                   for i in range(0, len(toks), 512)])
+    model.encode_tokens(toks[:8], device=dev)
+    if dev == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    bits = model.encode_tokens(toks, device=dev)
+    if dev == "cuda":
+        torch.cuda.synchronize()
+    out["encode_sequences_per_sec"] = a.decode_n / (time.perf_counter() - t0)
+    out["encode_bit_agreement_vs_torch"] = float((bits == ref_bits).mean())
+    if dev == "cuda":
+        # logits of the HIP encoder vs the fp32 eval-mode inference net: relative error, and bit
+        # disagreements whose torch margin exceeds 1 % of the mean |logit| (not bf16 rounding ties)
+        with torch.no_grad():
+            tt = torch.as_tensor(toks[:512], device=dev)
+            ref_l = model.inference_net(tt).float()
+            got_l = model._hip_encoder.logits(tt).float()
+        margin = (ref_l[..., 0] - ref_l[..., 1]).abs()
+        scale = ref_l.abs().mean()
+        out["encode_logits_rel_err"] = float((got_l - ref_l).norm() / ref_l.norm())
+        out["encode_margin_over_scale_median"] = float((margin / scale).median())
+        flips = (got_l.argmax(-1) != ref_l.argmax(-1))
+        out["encode_flips_with_margin_gt_1pct"] = int((flips & (margin > 0.01 * scale)).sum())
+
     print(json.dumps(out))
 
 
