@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--out", default="gpurun_out/bench_kernels.json")
     ap.add_argument("--only", type=str, default="", help="comma-separated launch indices to time (profiling)")
+    ap.add_argument("--ancestor-frac", type=float, default=0.0,
+                    help="fraction of clones of the example.json ancestor (table codec): the bench's regime")
     a = ap.parse_args()
     from serann.engine.hip_engine import HipPopulationEngine, Plan
     from serann.genome.codec import decoded_form
@@ -86,6 +88,14 @@ def main():
             irs.append(r.ir)
         if len(irs) == a.pop:
             break
+    if a.ancestor_frac > 0:
+        from serann.config import default_parameters
+        from serann.experiment.runner import build_codec
+        params = default_parameters("example")
+        codec = build_codec(params, "table", seed=0)
+        anc = try_interpret(codec.decode_to_string(np.asarray(params["ancestor_genotype"])[None])[0]).ir
+        k = int(round(a.ancestor_frac * a.pop))
+        irs = [anc] * k + irs[:a.pop - k]
     dev = torch.device("cuda")
     eng = HipPopulationEngine(irs, list(range(len(irs))), device=dev)
     B = a.batch

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--streams", default="4")
+    ap.add_argument("--ancestor-frac", type=float, default=0.0,
+                    help="fraction of the population that are clones of the example.json ancestor (table codec), "
+                         "as in the bench's evolved generations")
     a = ap.parse_args()
     from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
     from serann.engine.base import TrainConfig
@@ -37,6 +40,14 @@ def main():
             irs.append(r.ir)
         if len(irs) == a.pop:
             break
+    if a.ancestor_frac > 0:
+        from serann.config import default_parameters
+        from serann.experiment.runner import build_codec
+        params = default_parameters("example")
+        codec = build_codec(params, "table", seed=0)
+        anc = try_interpret(codec.decode_to_string(np.asarray(params["ancestor_genotype"])[None])[0]).ir
+        k = int(round(a.ancestor_frac * a.pop))
+        irs = [anc] * k + irs[:a.pop - k]
     data = get_serann_data(synthetic_encodings(), synthetic_mnist())
     for ns in a.streams.split(","):
         os.environ["SERANN_STREAMS"] = ns

@@ -335,6 +335,22 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
             }
         }
         __syncthreads();
+        if ((C & (C - 1)) == 0 && C < 64) {
+            // power-of-two C < 64: slot s holds channel s mod C and 256 % C == 0, so every slot thread t
+            // sums (t, t + 256, ...; 8 of them) is channel t mod C; lanes of equal t mod C then combine by
+            // xor shuffles.  All 256 threads share the 2048-slot gather (the per-channel loop below leaves
+            // C threads walking 2048 / C slots each: 256 serial LDS reads at C = 8).
+            const int lane = t & 63;
+            float a = 0.f, b = 0.f;
+#pragma unroll
+            for (int s = t; s < 2048; s += 256) { a += r0[s]; b += r1[s]; }
+            for (int o = C; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+            if (lane < C) {
+                atomicAdd(&ws[lane], a);
+                atomicAdd(&ws[C + lane], b);
+            }
+            return;
+        }
         for (int c = t; c < C; c += 256) {
             float a = 0.f, b = 0.f;
             for (int g = 0; g < G; ++g)
@@ -825,8 +841,8 @@ void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t
 }
 
 // ------------------------------------------------------------------------------------------------
-// Split-K finalize of the LDS-tiled FWD GEMM (GF_SPLITWS): out[m][n] = bf16(act(sum_s ws[s][m][n] +
-// bias[n])).  Grouped: tiles (problem, chunk of SPLITFIN_ELEMS outputs).
+// Split-K finalize of the LDS-tiled FWD GEMM (GF_SPLITWS): out[m][n] = act(sum_s ws[s][m][n] + bias[n]),
+// bf16 (or fp32 with flags & 1: the heads).  Grouped: tiles (problem, chunk of SPLITFIN_ELEMS outputs).
 constexpr int SPLITFIN_ELEMS = 2048;
 
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(const SplitFinDesc* __restrict__ descs,
@@ -838,13 +854,17 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const SplitFinDesc
     const float* __restrict__ ws = reinterpret_cast<const float*>(d.ws);
     const float* __restrict__ bias = reinterpret_cast<const float*>(d.bias);
     bf16_t* __restrict__ out = reinterpret_cast<bf16_t*>(d.out);
+    float* __restrict__ out32 = reinterpret_cast<float*>(d.out);
+    const bool f32 = d.flags & 1;
     const int64_t e0 = (int64_t)td.y * SPLITFIN_ELEMS;
     const int64_t e1 = min(MN, e0 + SPLITFIN_ELEMS);
     for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
         float v = 0.f;
         for (int s_ = 0; s_ < S; ++s_) v += ws[s_ * MN + e];
         if (bias) v += bias[(int)(e % N)];
-        out[e] = f2bf(apply_act(v, act));
+        v = apply_act(v, act);
+        if (f32) out32[e] = v;
+        else out[e] = f2bf(v);
     }
 }
 

@@ -660,6 +660,7 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     }
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     float* out = reinterpret_cast<float*>(d.out);
+    const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
 #pragma unroll
     for (int i = 0; i < TF; ++i)
 #pragma unroll
@@ -671,8 +672,8 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
                 if (row < g.M) {
                     // GF_WSTORE: this block is the problem's only m-split -> the sole writer
-                    if (g.flags & GF_WSTORE) out[(int64_t)row * g.N + col] = acc[i][j][r];
-                    else atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = acc[i][j][r];
+                    else atomicAdd(out + (int64_t)row * ldo + col, acc[i][j][r]);
                 }
             }
         }
@@ -1231,7 +1232,8 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const int64_t a_elems = (int64_t)M * lda;
     const rsrc_t rA = mkrsrc(d.a, a_elems * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? a_elems * 2 : 0);
-    const rsrc_t rB = mkrsrc(d.b, (int64_t)N * K * 2);
+    const int ldb = d.ldb ? (int)d.ldb : K;          // B row stride (a K slice of a wider weight matrix)
+    const rsrc_t rB = mkrsrc(d.b, (int64_t)N * ldb * 2);
     const uint4 zero = make_uint4(0, 0, 0, 0);
     const int gact = (MODE == MODE_DGRAD) ? act : ACT_LINEAR;
 
@@ -1254,7 +1256,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
         for (int i = 0; i < BPT; ++i) {
             const int n = n0 + lr + 64 * i;
-            const int off = (n < N && run > 0) ? n * K + k : -1;
+            const int off = (n < N && run > 0) ? n * ldb + k : -1;
             uint4 v = bl16(rB, off);
             if (run < 8) v = splice(v, zero, run);
             rb[i] = v;
@@ -1305,7 +1307,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const int rq = (lane >> 4) * 4;
     if (MODE == MODE_FWD && (flags & GF_SPLITWS)) {
         // raw fp32 partial of this k split; splitk_finalize adds the splits, bias and activation
-        float* w = reinterpret_cast<float*>(d.aux) + (int64_t)(kt0 / (int)d.kper) * M * N;
+        float* w = reinterpret_cast<float*>(d.aux) + ((int64_t)d.sbase + kt0 / (int)d.kper) * M * N;
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
             const int col = n0 + wc * (BN / 2) + j * 16 + r16;

@@ -14,7 +14,10 @@ struct GemmDesc {
     // divisors the v3 kernels need: q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31.
     int64_t dvC, dvKW, dvOW, dvOHW, dvF, dvW, dvHW, dvSH, dvSW;
     int64_t dvCp;     // magic of Cp = C rounded up to 8 (LDS-halo conv kernels)
-    int64_t kper;     // GF_SPLITWS: k steps (32) per split; split s writes aux + s * M * N (fp32)
+    int64_t kper;     // GF_SPLITWS: k steps (32) per split; split s writes aux + (sbase + s) * M * N (fp32)
+    int64_t ldb;      // LDS-tiled kernel: B row stride (0: K) -- a K slice [.., col0 + K) of a wider [N][ldb] matrix
+    int64_t sbase;    // GF_SPLITWS: first workspace slot of this problem (K slices of one output share a workspace)
+    int64_t ldo;      // WGRAD (64-row LDS kernel): output row stride (0: N) -- a column slice of a wider dW
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
@@ -67,7 +70,7 @@ struct BnDesc {
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
 struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
-struct SplitFinDesc { int64_t ws, out, bias, M, N, S, act, flags; };      // flags: reserved
+struct SplitFinDesc { int64_t ws, out, bias, M, N, S, act, flags; };      // flags: 1 = fp32 output
 struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;

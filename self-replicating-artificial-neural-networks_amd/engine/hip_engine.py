@@ -416,6 +416,55 @@ class HipPopulationEngine(PopulationEngine):
         off = rec["grad"].get(own)
         return None if off is None else mem["grad"].ptr(off)
 
+    def _fused_concats(self, mem, org_iter):
+        """Concatenations read in place by their consumers (no concat copy).
+
+        Eligible: a concat along the last axis whose every consumer (through reshapes) is a Dense /
+        classification-head GEMM that takes the concat's rows as its input rows -- the Keras pattern
+        ``Dense(concatenate([Reshape((1, -1))(X), Reshape((1, -1))(g)]))``.  The consumer then runs one
+        K slice per concat input (A = that input in place, B = its column range of the weights).
+        Returns (fcat[o]: concat id -> [(input id, first column, width)], fcons[o]: gemm id -> concat id).
+        SERANN_FUSE_CONCAT=0 turns it off."""
+        P = self.num_organisms
+        fcat = [dict() for _ in range(P)]
+        fcons = [dict() for _ in range(P)]
+        if os.environ.get("SERANN_FUSE_CONCAT", "1") == "0" or GEMM_IMPL != "v3":
+            return fcat, fcons
+        for o, lay in org_iter():
+            ir = lay.ir
+            owner = mem["orgs"][o]["owner"]
+            for c in ir.nodes:
+                if c.op != "concat" or owner.get(c.id) != c.id or c.attrs["axis"] != len(c.shape):
+                    continue
+                D, rows = c.shape[-1], math.prod(c.shape[:-1])
+                cons, ok = [], True
+                for n in ir.nodes:
+                    if n.op == "reshape" or not any(owner.get(i) == c.id for i in n.inputs):
+                        continue
+                    if n.op == "gemm" and n.attrs["kind"] == "head_rep":
+                        continue
+                    a = n.attrs
+                    if n.op == "gemm" and a["kind"] == "dense" and a["cin"] == D and a["h"] == rows:
+                        cons.append(n.id)
+                    elif n.op == "gemm" and a["kind"] == "head_cls" and ir.head_features == D and rows == 1:
+                        cons.append(n.id)
+                    else:
+                        ok = False
+                        break
+                if not ok or not cons:
+                    continue
+                parts, col = [], 0
+                for i in c.inputs:
+                    w = ir.node(i).shape[-1]
+                    parts.append((i, col, w))
+                    col += w
+                if col != D:
+                    continue
+                fcat[o][c.id] = parts
+                for g in cons:
+                    fcons[o][g] = c.id
+        return fcat, fcons
+
     def _stream_groups(self, nstreams: int) -> List[List[int]]:
         """Partition the organisms into <= nstreams groups of similar training FLOPs (LPT)."""
         P = self.num_organisms
@@ -466,14 +515,16 @@ class HipPopulationEngine(PopulationEngine):
             a = np.zeros(len(rows), dtype=dtype)
             for i, r in enumerate(rows):
                 for k, v in r.items():
-                    a[i][k] = v
+                    if not k.startswith("_"):
+                        a[i][k] = v
             if dtype == H.GEMM_DTYPE:
                 H.fill_gemm_divisors(a)
             return T(np.frombuffer(a.tobytes(), dtype=np.uint8).copy())
 
-        def add_gemm(mode_, rows, dims):
+        def add_gemm(mode_, rows, dims, extra_fin=None):
             if not rows:
                 return
+            assert len(rows) == len(dims), (len(rows), len(dims))
             if GEMM_IMPL == "v1":
                 if mode_ == H.MODE_DGRAD:
                     rows = [dict(r, b=r["b_v1"]) for r in rows]
@@ -492,7 +543,7 @@ class HipPopulationEngine(PopulationEngine):
                     fin = []
                     for r in rws:
                         ns = int(r.pop("_split", 1))
-                        if ns > 1:
+                        if ns > 1 and not r.get("_pre"):
                             wsb = torch.empty(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
                             plan.keep.append(wsb)
                             r["aux"] = wsb.data_ptr()
@@ -503,6 +554,10 @@ class HipPopulationEngine(PopulationEngine):
                     if fin:
                         add_chunked("splitfin", 0, fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in fin],
                                     H.SPLITFIN_ELEMS)
+                if extra_fin:
+                    # K slices of fused-concat consumers (every variant launched above): one finalize
+                    add_chunked("splitfin", 0, extra_fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in extra_fin],
+                                H.SPLITFIN_ELEMS)
                 return
             groups = {}
             for r, dm in zip(rows, dims):
@@ -570,8 +625,22 @@ class HipPopulationEngine(PopulationEngine):
 
         plan.imcol_lookup = raw_conv_imcol
 
+        fcat, fcons = self._fused_concats(mem, org_iter)
+
+        def concat_slices(o, n, F):
+            """K slices (input node, first column, width, k splits, first workspace slot) of a fused-concat
+            consumer, and the number of workspace slots."""
+            out, S = [], 0
+            for pid, col, width in fcat[o][fcons[o][n.id]]:
+                kt = -(-width // H.BK)
+                ns = max(1, min(16, kt // H.SPLIT_KSTEPS)) if H.SPLIT_KSTEPS > 0 else 1
+                out.append((pid, col, width, ns, S))
+                S += ns
+            return out, S
+
         # ---- forward ---------------------------------------------------------------------------
         for d in range(1, maxd + 1):
+            fin_rows = []
             g_rows, g_dims = [], []
             p_rows, p_cnt = [], []
             bn_rows, bn_cnt = [], []
@@ -607,7 +676,23 @@ class HipPopulationEngine(PopulationEngine):
                             flags |= H.GF_VEC_B
                         bias = pptr(lay.b[n.id]) if n.id in lay.b else 0
                         ic = raw_conv_imcol(o, n) if a["kind"] != "head_cls" else None
-                        if ic is not None:
+                        if n.id in fcons[o]:
+                            # consumer of a fused concat: one K slice per concat input, read in place
+                            # (no concat copy); fp32 partials + one finalize (bias, activation)
+                            D = ir.head_features if a["kind"] == "head_cls" else C
+                            sl, S = concat_slices(o, n, F)
+                            wsb = torch.empty(S * M * F, dtype=torch.float32, device=self.device)
+                            plan.keep.append(wsb)
+                            for pid, col, width, ns, sb in sl:
+                                g_rows.append(dict(a=self._act_ptr(mem, o, pid, inputs), b=wptr_bf(lay.w[n.id]) + 2 * col,
+                                                   out=out, bias=0, H=1, W=1, C=width, OH=1, OW=1, F=F, KH=1, KW=1,
+                                                   SH=1, SW=1, M=M, N=F, K=width, act=0, flags=0, ldb=D,
+                                                   aux=wsb.data_ptr(), sbase=sb, _split=ns, _ws=1, _force_tiled=1,
+                                                   _pre=1))
+                                g_dims.append((M, F, width))
+                            fin_rows.append(dict(ws=wsb.data_ptr(), out=out, bias=bias, M=M, N=F, S=S, act=act,
+                                                 flags=1 if a["kind"] == "head_cls" else 0))
+                        elif ic is not None:
                             g_rows.append(dict(a=ic["buf"].data_ptr(), b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=OH,
                                                W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=F,
                                                K=K, act=act, flags=flags))
@@ -615,7 +700,8 @@ class HipPopulationEngine(PopulationEngine):
                             g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
                                                OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
                                                flags=flags))
-                        g_dims.append((M, F, K))
+                        if n.id not in fcons[o]:
+                            g_dims.append((M, F, K))      # (K slices appended their own dims)
                     elif n.op == "pool":
                         p_rows.append(dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
                                            y=self._act_ptr(mem, o, n.id, inputs),
@@ -636,6 +722,8 @@ class HipPopulationEngine(PopulationEngine):
                                             flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
                         bn_cnt.append(H.bn_chunks(B * math.prod(n.shape) // c, c))
                     elif n.op == "concat":
+                        if n.id in fcat[o]:
+                            continue                  # read in place by its consumers' K slices
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])
                         out_inner = math.prod(n.shape[ax - 1:])
@@ -650,7 +738,7 @@ class HipPopulationEngine(PopulationEngine):
                             col += inner
                     else:
                         fallbacks.append((o, n))
-            add_gemm(H.MODE_FWD, g_rows, g_dims)
+            add_gemm(H.MODE_FWD, g_rows, g_dims, extra_fin=fin_rows)
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             if bn_rows:
                 if train:
@@ -759,6 +847,26 @@ class HipPopulationEngine(PopulationEngine):
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
                         ic = raw_conv_imcol(o, n) if fused and not head else None
+                        if fused and n.id in fcons[o]:
+                            # fused-concat consumer: WGRAD and DGRAD per K slice, in place on the concat
+                            # inputs and their gradient buffers (no concat copy, no DGRAD for inputs
+                            # without a gradient, e.g. the raw image)
+                            D = C
+                            sl, _ = concat_slices(o, n, F)
+                            for q, (pid, col, width, ns, sb) in enumerate(sl):
+                                wg_rows.append(dict(a=dz, b=self._act_ptr(mem, o, pid, inputs), out=gptr(lay.w[n.id]) + 4 * col,
+                                                    bias=dbias if q == 0 else 0, aux=yv, act=act, H=Hh, W=1, C=width,
+                                                    OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=F, N=width, K=M,
+                                                    flags=(H.GF_VEC_A if F % 8 == 0 else 0), ldo=D, _nonarrow=1))
+                                wg_dims.append((F, width, M))
+                                own_p = target(o, pid)
+                                if own_p is not None:
+                                    base = dict(a=dz, b=self.wt.data_ptr() + 2 * (self.wt_off[o][n.id] + col * F), b_v1=0,
+                                                aux=yv, act=act, out=mem["grad"].ptr(rec["grad"][own_p]), H=Hh, W=1,
+                                                C=width, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=width, K=F)
+                                    tasks["dgrad"].append((o, own_p, lambda acc, r=base: dict(r, flags=H.GF_ACCUM if acc else 0),
+                                                           (M, width, F)))
+                            continue
                         if ic is not None:
                             wg_rows.append(dict(a=dz, b=ic["buf"].data_ptr(), out=gptr(lay.w[n.id]), bias=dbias,
                                                 aux=yv, act=act, H=OH, W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1,
@@ -816,6 +924,8 @@ class HipPopulationEngine(PopulationEngine):
                             tasks["bn"].append((o, own, lambda acc, r=base, f=pflags: dict(r, flags=f | (4 if acc else 0)),
                                                 H.bn_chunks(R, c)))
                     elif n.op == "concat":
+                        if n.id in fcat[o]:
+                            continue                  # its consumers' DGRAD slices wrote the input gradients
                         ax = a["axis"]
                         outer = B * math.prod(n.shape[:ax - 1])
                         out_inner = math.prod(n.shape[ax - 1:])

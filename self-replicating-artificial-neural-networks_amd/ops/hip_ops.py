@@ -15,7 +15,10 @@ GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "
                "M", "N", "K", "act", "flags",
                # fast-division magics for the v3 kernels (filled by fill_gemm_divisors)
                "dvC", "dvKW", "dvOW", "dvOHW", "dvF", "dvW", "dvHW", "dvSH", "dvSW", "dvCp",
-               "kper"]      # GF_SPLITWS: k steps per split
+               "kper",      # GF_SPLITWS: k steps per split
+               "ldb",       # LDS-tiled kernel: B row stride (0: K)
+               "sbase",     # GF_SPLITWS: first workspace slot
+               "ldo"]       # 64-row WGRAD: output row stride (0: N)
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 ACTBWD_DTYPE = np.dtype([(f, _I) for f in ["dy", "y", "dz", "dbias", "M", "N", "act", "flags"]])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
@@ -69,7 +72,8 @@ def gemm_desc_array(rows) -> np.ndarray:
     a = np.zeros(len(rows), dtype=GEMM_DTYPE)
     for i, r in enumerate(rows):
         for k, v in r.items():
-            a[i][k] = v
+            if not k.startswith("_"):
+                a[i][k] = v
     return fill_gemm_divisors(a)
 
 
@@ -270,8 +274,10 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     for r, dm in zip(rows, dims):
         M, N, K = dm
         v = None
-        nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) else None
-        if nk is not None:
+        nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) and not r.get("_nonarrow") else None
+        if r.get("_force_tiled"):
+            v = 7128 if N > 64 else 7064          # K slice of a concat input: LDS-tiled + workspace
+        elif nk is not None:
             v = (6000 if mode == MODE_FWD else 4000000) + nk
         elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
               and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
@@ -347,8 +353,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                     kt = -(-K // BK)
                     ns = int(r.get("_split", 1))
                     per = -(-kt // ns)
-                    if ns > 1:
-                        r["kper"] = per
+                    if ns > 1 or r.get("_ws"):
+                        r["kper"] = max(per, 1)
                         r["flags"] = int(r.get("flags", 0)) | GF_SPLITWS
                     t = gemm_tiles([(M, N, K)], mode, bm=bm, bn=bn)
                     for s_ in range(ns):

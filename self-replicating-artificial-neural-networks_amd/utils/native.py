@@ -17,8 +17,12 @@ def load(name: str, required: bool = False):
     if name in _cache:
         return _cache[name]
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    # SERANN_NATIVE_DIR: load the extensions of another in-tree build (A/B timing of two kernel versions)
-    path = Path(os.environ.get("SERANN_NATIVE_DIR") or NATIVE_DIR) / f"{name}{suffix}"
+    # SERANN_NATIVE_DIR: load the extensions of another in-tree build (A/B timing of two kernel versions);
+    # an extension that directory does not hold comes from the in-tree build
+    path = NATIVE_DIR / f"{name}{suffix}"
+    alt = os.environ.get("SERANN_NATIVE_DIR")
+    if alt and (Path(alt) / f"{name}{suffix}").exists():
+        path = Path(alt) / f"{name}{suffix}"
     mod = None
     if path.exists():
         if name.startswith("serann_hip"):
