@@ -1207,12 +1207,18 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
 // Rows of 40 elements (80 B, an odd number of 16-B slots) keep the 16-row ds_read_b128 fragment reads
 // conflict-free.  The epilogue stages the block's tile in LDS and streams it out with 16-B stores
 // when the block spans all N columns (the usual case: N <= 128).
-template <int MODE, int BN>
+// BT (DGRAD only): B is the layer's weight matrix in its natural [K = F][N = C] layout (row stride ldb,
+// default N) instead of the transposed copy Wt[C][F]: a k-step's B tile is loaded as 32 k rows x BN
+// columns (16-B chunks along n), staged k-major in LDS ([32][BN + 8]) and its MFMA fragments are read
+// with ds_read_b64_tr_b16 (lane i of a 16-lane group receives column i of 4 consecutive k rows, k row q
+// in element q -- the k order of the ds_read_b128 A fragments).  No per-step weight transpose launch.
+template <int MODE, int BN, bool BT = false>
 __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restrict__ descs,
                                                        const int4* __restrict__ tiles) {
     constexpr int BM = 128, BK = 32, LDS_ROW = BK + 8;
     constexpr int NTW = BN / 32;                     // 16-col tiles per wave (2 waves along n)
-    constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = 2 * BN * LDS_ROW;
+    constexpr int LDBT = BN + 8;                     // BT: k-major B row (multiple of 8 elements)
+    constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = BT ? 2 * BK * LDBT : 2 * BN * LDS_ROW;
     constexpr int STAGE = BM * BN;                   // epilogue staging (bf16 elements)
     constexpr int LDSN = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
     __shared__ __attribute__((aligned(16))) bf16_t lds[LDSN];
@@ -1232,15 +1238,19 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const int64_t a_elems = (int64_t)M * lda;
     const rsrc_t rA = mkrsrc(d.a, a_elems * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? a_elems * 2 : 0);
-    const int ldb = d.ldb ? (int)d.ldb : K;          // B row stride (a K slice of a wider weight matrix)
-    const rsrc_t rB = mkrsrc(d.b, (int64_t)N * ldb * 2);
+    // B row stride: a K slice of a wider weight matrix (FWD), or the natural [K][N] weights (BT)
+    const int ldb = d.ldb ? (int)d.ldb : (BT ? N : K);
+    const rsrc_t rB = mkrsrc(d.b, (int64_t)(BT ? K : N) * ldb * 2);
     const uint4 zero = make_uint4(0, 0, 0, 0);
     const int gact = (MODE == MODE_DGRAD) ? act : ACT_LINEAR;
 
     // loaders: thread t -> (row t/4 + 64 i, k chunk (t % 4) * 8)
     const int lr = t >> 2, lk = (t & 3) * 8;
     constexpr int BPT = BN / 64;                     // B chunks per thread
-    uint4 ra[2], rb[BPT];
+    // BT loader: thread t -> (k row t / NCH + BKP i, n chunk (t % NCH) * 8)
+    constexpr int NCH = BN / 8, BKP = 256 / NCH, BTP = BK / BKP;
+    const int bkr = t / NCH, bnc = (t % NCH) * 8;
+    uint4 ra[2], rb[BT ? BTP : BPT];
     auto gload = [&](int kt) {
         const int k = kt * BK + lk;
         const int run = min(8, K - k);
@@ -1253,22 +1263,40 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             if (run < 8) v = splice(v, zero, run);
             ra[i] = v;
         }
+        if (BT) {
 #pragma unroll
-        for (int i = 0; i < BPT; ++i) {
-            const int n = n0 + lr + 64 * i;
-            const int off = (n < N && run > 0) ? n * ldb + k : -1;
-            uint4 v = bl16(rB, off);
-            if (run < 8) v = splice(v, zero, run);
-            rb[i] = v;
+            for (int i = 0; i < BTP; ++i) {
+                const int kk = kt * BK + bkr + BKP * i;
+                const int n = n0 + bnc;
+                const int off = (kk < K && n < N) ? kk * ldb + n : -1;
+                uint4 v = bl16(rB, off);
+                if (N - n < 8) v = splice(v, zero, N - n);
+                rb[i] = v;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < BPT; ++i) {
+                const int n = n0 + lr + 64 * i;
+                const int off = (n < N && run > 0) ? n * ldb + k : -1;
+                uint4 v = bl16(rB, off);
+                if (run < 8) v = splice(v, zero, run);
+                rb[i] = v;
+            }
         }
     };
     auto sstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lk]) = ra[i];
+        if (BT) {
 #pragma unroll
-        for (int i = 0; i < BPT; ++i)
-            *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
+            for (int i = 0; i < BTP; ++i)
+                *reinterpret_cast<uint4*>(&Bs[(buf * BK + bkr + BKP * i) * LDBT + bnc]) = rb[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < BPT; ++i)
+                *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
+        }
     };
 
     f32x4_t acc[4][NTW];
@@ -1289,9 +1317,23 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             fa[i].u = *reinterpret_cast<const uint4*>(&As[(buf * BM + wr * 64 + i * 16 + r16) * LDS_ROW + kg]);
+        if (BT) {
+            const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
-        for (int j = 0; j < NTW; ++j)
-            fb[j].u = *reinterpret_cast<const uint4*>(&Bs[(buf * BN + wc * (BN / 2) + j * 16 + r16) * LDS_ROW + kg]);
+            for (int j = 0; j < NTW; ++j) {
+                const int colb = wc * (BN / 2) + j * 16 + 4 * pp;
+                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(buf * BK + grp * 8 + q) * LDBT + colb]));
+                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(buf * BK + grp * 8 + 4 + q) * LDBT + colb]));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { fb[j].h[e] = (bf16_t)lo[e]; fb[j].h[4 + e] = (bf16_t)hi[e]; }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NTW; ++j)
+                fb[j].u = *reinterpret_cast<const uint4*>(&Bs[(buf * BN + wc * (BN / 2) + j * 16 + r16) * LDS_ROW + kg]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1401,7 +1443,8 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
 //                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4),
-//                 7064 / 7128 for the LDS-tiled 1x1 kernel (BN = 64 / 128; tiles (prob, m tile, n tile, k range))
+//                 7064 / 7128 for the LDS-tiled 1x1 kernel (BN = 64 / 128; tiles (prob, m tile, n tile, k range)),
+//                 8064 / 8128 the same for DGRAD with B = natural-layout weights [F][C] (BT)
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
@@ -1471,6 +1514,12 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else if (mode == MODE_FWD) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, 128>), grid, block, 0, s, dp, tp);
         else if (variant == 7064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 64>), grid, block, 0, s, dp, tp);
         else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128>), grid, block, 0, s, dp, tp);
+        SERANN_CHECK(hipGetLastError());
+        return;
+    }
+    if (mode == MODE_DGRAD && (variant == 8064 || variant == 8128)) {   // BT: natural-layout weights
+        if (variant == 8064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 64, true>), grid, block, 0, s, dp, tp);
+        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128, true>), grid, block, 0, s, dp, tp);
         SERANN_CHECK(hipGetLastError());
         return;
     }

@@ -799,6 +799,14 @@ class HipPopulationEngine(PopulationEngine):
                         F_, P_, C_ = ir.num_classes + ir.genotype_size, 1, ir.head_features
                     else:
                         F_, P_, C_ = a["f"], a["kh"] * a["kw"], a["cin"]
+                    # the transposed copy Wt[C][KH][KW][F] only feeds DGRAD kernels that cannot read the
+                    # natural layout, and only layers whose input needs a gradient have a DGRAD at all
+                    if nid in fcons[o]:
+                        needs_dgrad = any(target(o, pid) is not None for pid, _, _ in fcat[o][fcons[o][nid]])
+                    else:
+                        needs_dgrad = target(o, ir.node(nid).inputs[0]) is not None
+                    if not needs_dgrad or H.dgrad_reads_natural(a["kh"], a["kw"], a["sh"], a["sw"], F_):
+                        continue
                     trows.append(dict(src=wptr_bf(off), dst=self.wt.data_ptr() + 2 * self.wt_off[o][nid], F=F_, P=P_,
                                       C=C_))
                     tcnt.append(-(-(F_ * P_ * C_) // H.TRANS_ELEMS))
@@ -862,6 +870,7 @@ class HipPopulationEngine(PopulationEngine):
                                 own_p = target(o, pid)
                                 if own_p is not None:
                                     base = dict(a=dz, b=self.wt.data_ptr() + 2 * (self.wt_off[o][n.id] + col * F), b_v1=0,
+                                                _bnat=wptr_bf(lay.w[n.id]) + 2 * col, _bnat_ld=D,
                                                 aux=yv, act=act, out=mem["grad"].ptr(rec["grad"][own_p]), H=Hh, W=1,
                                                 C=width, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=width, K=F)
                                     tasks["dgrad"].append((o, own_p, lambda acc, r=base: dict(r, flags=H.GF_ACCUM if acc else 0),
@@ -886,6 +895,7 @@ class HipPopulationEngine(PopulationEngine):
                         if own is not None:
                             Mi = B * Hh * Ww
                             base = dict(a=dz, b=self.wt.data_ptr() + 2 * self.wt_off[o][n.id], b_v1=wptr_bf(lay.w[n.id]),
+                                        _bnat=wptr_bf(lay.w[n.id]),
                                         aux=yv if fused else 0, act=act if fused else 0,
                                         out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
                                         W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,

@@ -185,6 +185,8 @@ def gemm3_block(mode: int, variant: int):
         return (v // 1000, v % 1000)
     if variant in (7064, 7128):
         return (128, variant - 7000)
+    if variant in (8064, 8128):
+        return (128, variant - 8000)
     if variant >= 5000:
         return (64 * ((variant // 10) % 10), 16 * (variant % 10))
     nt, rt, kw = variant % 10, (variant // 10) % 10, (variant % 1000) >= 100
@@ -282,6 +284,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
         elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
               and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
             v = 7128 if N > 64 else 7064          # LDS-tiled 1x1 / Dense GEMM
+            if mode == MODE_DGRAD and r.get("_bnat") and "bt" not in _OFF:
+                # natural-layout weights read k-major (no transposed copy needed)
+                v += 1000
+                r["b"] = r["_bnat"]
+                r["ldb"] = int(r.get("_bnat_ld", 0))
             if mode == MODE_FWD and splitk:
                 ns = tiled_fwd_splits(M, N, K, v - 7000, int(r.get("flags", 0)))
                 if ns > 1:
@@ -370,6 +377,12 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tiles = gemm_tiles(dms, mode, bm=bm, bn=bn)
         out.append((v, [r for r, _ in items], tiles))
     return out
+
+
+def dgrad_reads_natural(KH: int, KW: int, SH: int, SW: int, F: int) -> bool:
+    """True when a layer's DGRAD runs on the LDS-tiled kernel reading the natural [F][C] weights (BT,
+    variants 8064 / 8128), i.e. it needs no transposed weight copy (mirrors gemm3_plan)."""
+    return ("tiled" not in _OFF and "bt" not in _OFF and KH * KW == 1 and SH * SW == 1 and F > BK)
 
 
 SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "48"))   # target k steps per split (0: off)

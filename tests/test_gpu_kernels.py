@@ -165,6 +165,36 @@ def test_tiled_fwd_split_k_with_finalize():
         assert _rel(y.float(), r) < 6e-3
 
 
+@pytest.mark.parametrize("M,N,F,D,col,act", [(750, 300, 152, 300, 0, "relu"), (96, 77, 40, 77, 0, "sigmoid"),
+                                               (64, 130, 33, 130, 0, "linear"), (200, 57, 110, 200, 100, "relu")])
+def test_tiled_dgrad_natural_weights(M, N, F, D, col, act):
+    """Dense DGRAD on the LDS-tiled kernel reading the natural [F][D] weights k-major (BT variant, no
+    transposed copy), optionally a column slice [col, col + N) of a wider weight matrix (fused concat),
+    with dZ = dY * act'(Y) fused on load."""
+    torch.cuda.synchronize()
+    dy = torch.randn(M, F, device=DEV).bfloat16()
+    y = torch.randn(M, F, device=DEV).bfloat16()
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "sigmoid":
+        y = torch.sigmoid(y.float()).bfloat16()
+    w = (torch.randn(F, D, device=DEV) / math.sqrt(F)).bfloat16()
+    dx = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    row = dict(a=dy.data_ptr(), b=0, _bnat=w.data_ptr() + 2 * col, _bnat_ld=D, aux=y.data_ptr(), act=H.ACT_CODES[act],
+               out=dx.data_ptr(), H=1, W=1, C=N, OH=1, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=F, flags=0)
+    plans = H.gemm3_plan(H.MODE_DGRAD, [row], [(M, N, F)])
+    assert [v for v, _, _ in plans] == [8128 if N > 64 else 8064]
+    for v, rws, tiles in plans:
+        d = _desc([{k: val for k, val in r.items() if not k.startswith("_")} for r in rws], H.GEMM_DTYPE)
+        t = torch.as_tensor(tiles, device=DEV)
+        H.lib().gemm3(H.MODE_DGRAD, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    torch.cuda.synchronize()
+    yf = y.float()
+    g = {"relu": (yf > 0).float(), "sigmoid": yf * (1 - yf), "linear": torch.ones_like(yf)}[act]
+    ref = (dy.float() * g) @ w.float()[:, col:col + N]
+    assert _rel(dx.float(), ref) < 6e-3
+
+
 def test_transpose_weights_kernel():
     w = torch.randn(37, 3, 5, 13, device=DEV).bfloat16()
     out = torch.zeros(13, 3, 5, 37, dtype=torch.bfloat16, device=DEV)
