@@ -155,6 +155,7 @@ __device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const 
 // partial sums, per-channel combination through LDS float atomics, one global atomic per channel
 // and block.  Works for any C (odd channel counts included).
 constexpr int BN_VEC_ELEMS = 16384;     // elements per block (super-rows per block = 2048 / C)
+constexpr int BN_RED_MULT = 4;          // statistics phases: BN_RED_MULT x BN_VEC_ELEMS per block
 
 __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, float* sA, float* sB) {
     const int R = (int)d.R, C = (int)d.C;
@@ -165,7 +166,9 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     const int G = 256 / C;                       // super-rows processed together
     const bool active = t < G * C;
     const int q = t / C, i = t - q * C;
-    const int srb = max(1, (BN_VEC_ELEMS / 8) / C);
+    // the statistics phases (0, 4) walk BN_RED_MULT times more rows per block: every block ends with
+    // 2C device-scope float atomics, which dominated those phases at 16K elements per block
+    const int srb = max(1, (BN_VEC_ELEMS / 8) / C) * ((phase == 0 || phase == 4) ? BN_RED_MULT : 1);
     const int nsr = (R + 7) / 8;
     const int sr0 = tile * srb, sr1 = min(nsr, sr0 + srb);
     const int64_t total = (int64_t)R * C;

@@ -643,7 +643,7 @@ class HipPopulationEngine(PopulationEngine):
             fin_rows = []
             g_rows, g_dims = [], []
             p_rows, p_cnt = [], []
-            bn_rows, bn_cnt = [], []
+            bn_rows, bn_cnt, bn_cnt_st = [], [], []
             c_rows, c_cnt = [], []
             fallbacks = []
             for o, lay in org_iter():
@@ -721,6 +721,7 @@ class HipPopulationEngine(PopulationEngine):
                                             ws=mem["ws"].ptr(bd["ws"]), R=B * math.prod(n.shape) // c, C=c,
                                             flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
                         bn_cnt.append(H.bn_chunks(B * math.prod(n.shape) // c, c))
+                        bn_cnt_st.append(H.bn_chunks(B * math.prod(n.shape) // c, c, stats=True))
                     elif n.op == "concat":
                         if n.id in fcat[o]:
                             continue                  # read in place by its consumers' K slices
@@ -742,7 +743,7 @@ class HipPopulationEngine(PopulationEngine):
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             if bn_rows:
                 if train:
-                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt, 1)
+                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt_st, 1)
                     add_chunked("bn", 2, bn_rows, H.BN_DTYPE, bn_cnt, 1)
                 else:
                     add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, 1)
@@ -926,7 +927,7 @@ class HipPopulationEngine(PopulationEngine):
                                     dbeta=gptr(lay.beta[n.id]) if n.id in lay.beta else 0,
                                     R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
                         bn_red.append(dict(base, flags=pflags))
-                        bn_red_cnt.append(H.bn_chunks(R, c))
+                        bn_red_cnt.append(H.bn_chunks(R, c, stats=True))
                         if own is None:
                             tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
                                                 H.bn_chunks(R, c)))

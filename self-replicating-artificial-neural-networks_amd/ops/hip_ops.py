@@ -80,12 +80,16 @@ def gemm_desc_array(rows) -> np.ndarray:
 BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256) BatchNorm kernel
 
 
-def bn_chunks(rows: int, channels: int) -> int:
-    """Blocks of a BatchNorm problem [rows][channels] (aux.hip bn_kernel chunking)."""
+BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block
+
+
+def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
+    """Blocks of a BatchNorm problem [rows][channels] (aux.hip bn_kernel chunking); ``stats``: a
+    statistics phase (0 or 4)."""
     c = max(int(channels), 1)
     if c > 256:
         return red_chunks(rows, c)
-    srb = max(1, (BN_VEC_ELEMS // 8) // c)
+    srb = max(1, (BN_VEC_ELEMS // 8) // c) * (BN_RED_MULT if stats else 1)
     return -(-(-(-int(rows) // 8)) // srb)
 
 

@@ -245,9 +245,11 @@ def test_bn_train_infer_backward(RC):
                ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
     d = _desc([row], H.BN_DTYPE)
     t = torch.as_tensor(H.chunk_tiles([H.bn_chunks(R, C)], 1), device=DEV)
+    ts = torch.as_tensor(H.chunk_tiles([H.bn_chunks(R, C, stats=True)], 1), device=DEV)   # phases 0 / 4
     L, s = H.lib(), H.stream_handle()
     for ph in (0, 2):
-        L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
+        tt = ts if ph == 0 else t
+        L.bn(ph, d.data_ptr(), tt.data_ptr(), len(tt), s)
     torch.cuda.synchronize()
     xf = x.float().requires_grad_(True)
     g_ = gamma.clone().requires_grad_(True)
@@ -260,7 +262,8 @@ def test_bn_train_infer_backward(RC):
     # backward (workspace re-zeroed, as the engine's per-step memset does)
     ws.zero_()
     for ph in (4, 5):
-        L.bn(ph, d.data_ptr(), t.data_ptr(), len(t), s)
+        tt = ts if ph == 4 else t
+        L.bn(ph, d.data_ptr(), tt.data_ptr(), len(tt), s)
     torch.cuda.synchronize()
     ref.backward(dy.float())
     assert _rel(dx.float(), xf.grad) < 1e-2
