@@ -168,6 +168,7 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
         bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
         if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
             return 64 * 1000 + 16 + (1000000 if im2col_gen else 0)
+
         if bmf == 16:
             bnk = 256 if N > 128 else (128 if N > 64 else 64)
         else:
