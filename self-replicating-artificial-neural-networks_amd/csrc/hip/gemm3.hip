@@ -1055,7 +1055,11 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
 constexpr int NARROW_ROWS = 256;        // FWD rows per block
 constexpr int NARROW_WROWS = 1024;      // WGRAD rows per block
 
-template <int K>
+// ST (output channels N % 8 != 0, e.g. Dense(units=75) on the raw genotype): the rows are computed
+// into an LDS tile and leave as one contiguous range with 16-B stores -- the row stride N is not a
+// multiple of 8, so per-thread 16-B row chunks are not aligned and the plain path stores 2-B elements.
+constexpr int NARROW_SROWS = 64;        // FWD staged pass (rows): 64 x N (<= 256) bf16 = <= 32 KB
+template <int K, bool ST>
 __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
     const int4 td = tiles[blockIdx.x];
@@ -1065,7 +1069,8 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     const int FC = (N + 7) >> 3;                 // 8-channel chunks per row (<= 32: N <= 256)
     const int RPI = 256 / FC;
     const int t = threadIdx.x;
-    if (t >= RPI * FC) return;
+    const bool active = t < RPI * FC;
+    if (!ST && !active) return;
     const int chunk = t % FC, rl = t / FC;
     const int f0 = chunk * 8;
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.a);
@@ -1083,6 +1088,45 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     const bool vec = (N & 7) == 0;
     const int r0 = td.y * NARROW_ROWS, r1 = min(M, r0 + NARROW_ROWS);
     constexpr int U = 4;                         // rows in flight per thread
+    if constexpr (ST) {
+        __shared__ __attribute__((aligned(16))) bf16_t st[NARROW_SROWS * 256];
+        for (int p0 = r0; p0 < r1; p0 += NARROW_SROWS) {
+            const int p1 = min(r1, p0 + NARROW_SROWS);
+            if (active) {
+                for (int rb = p0 + rl; rb < p1; rb += U * RPI) {
+                    float xv[U][K];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int r = min(rb + u * RPI, p1 - 1);
+#pragma unroll
+                        for (int k = 0; k < K; ++k) xv[u][k] = bf2f(X[(int64_t)r * ldx + k]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int r = rb + u * RPI;
+                        if (r >= p1) break;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            if (f0 + j >= N) break;
+                            float v = bv[j];
+#pragma unroll
+                            for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
+                            st[(r - p0) * N + f0 + j] = f2bf(apply_act(v, act));
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            // rows [p0, p1) are one contiguous range; p0 * N * 2 B is a multiple of 128 B
+            const int total = (p1 - p0) * N, nvec = total >> 3;
+            bf16_t* __restrict__ dst = Y + (int64_t)p0 * N;
+            for (int v = t; v < nvec; v += 256)
+                *reinterpret_cast<uint4*>(dst + 8 * v) = *reinterpret_cast<const uint4*>(&st[8 * v]);
+            for (int e = nvec * 8 + t; e < total; e += 256) dst[e] = st[e];
+            __syncthreads();
+        }
+        return;
+    }
     for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
         float xv[U][K];
 #pragma unroll
@@ -1115,7 +1159,11 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     }
 }
 
-template <int K>
+// ST (F % 8 != 0): dY / Y rows are staged through LDS 16 rows at a time with contiguous 16-B loads (the
+// plain path loads 2-B elements when the row stride F is not a multiple of 8); the staging buffers alias
+// the reduction array, which is used only after the row loop.
+constexpr int NARROW_WSROWS = 16;
+template <int K, bool ST>
 __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                               const int4* __restrict__ tiles) {
     // WGRAD dims: M = F (rows of dW), N = K (columns), K = reduction rows; dZ = dY * act'(Y)
@@ -1140,7 +1188,46 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
     for (int j = 0; j < NA; ++j) acc[j] = 0.f;
     const bool vec = (F & 7) == 0;
     const int r0 = td.y * NARROW_WROWS, r1 = min(R, r0 + NARROW_WROWS);
-    if (active) {
+    if constexpr (ST) {
+        static_assert(2 * NARROW_WSROWS * 256 * 2 <= 256 * NA * 4, "staging must fit in the reduction array");
+        bf16_t* sg = reinterpret_cast<bf16_t*>(red);
+        bf16_t* sy = sg + NARROW_WSROWS * 256;
+        for (int p0 = r0; p0 < r1; p0 += NARROW_WSROWS) {
+            const int p1 = min(r1, p0 + NARROW_WSROWS);
+            const int total = (p1 - p0) * F, nvec = total >> 3;
+            // p0 * F * 2 B is a multiple of 32 B: aligned 16-B loads of the contiguous row range
+            const bf16_t* gsrc = dY + (int64_t)p0 * F;
+            const bf16_t* ysrc = Yv + (int64_t)p0 * F;
+            for (int v = t; v < nvec; v += 256) {
+                *reinterpret_cast<uint4*>(&sg[8 * v]) = *reinterpret_cast<const uint4*>(gsrc + 8 * v);
+                if (act != ACT_LINEAR)
+                    *reinterpret_cast<uint4*>(&sy[8 * v]) = *reinterpret_cast<const uint4*>(ysrc + 8 * v);
+            }
+            for (int e = nvec * 8 + t; e < total; e += 256) {
+                sg[e] = gsrc[e];
+                if (act != ACT_LINEAR) sy[e] = ysrc[e];
+            }
+            __syncthreads();
+            if (active) {
+                for (int r = p0 + rl; r < p1; r += RPI) {
+                    float xv[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) xv[k] = bf2f(X[(int64_t)r * ldx + k]);
+                    const int base = (r - p0) * F + f0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (f0 + j >= F) break;
+                        float gz = bf2f(sg[base + j]);
+                        if (act != ACT_LINEAR) gz = bf2f(f2bf(gz * act_grad_from_y(bf2f(sy[base + j]), act)));
+#pragma unroll
+                        for (int k = 0; k < K; ++k) acc[j * K + k] += gz * xv[k];
+                        acc[8 * K + j] += gz;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    } else if (active) {
         constexpr int U = 4;                     // rows in flight per thread
         for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
             union V8 { uint4 u; bf16_t h[8]; };
@@ -1221,7 +1308,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     constexpr int NTW = BN / 32;                     // 16-col tiles per wave (2 waves along n)
     constexpr int LDBT = BN + 8;                     // BT: k-major B row (multiple of 8 elements)
     constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = BT ? 2 * BK * LDBT : 2 * BN * LDS_ROW;
-    constexpr int STAGE = BM * BN;                   // epilogue staging (bf16 elements)
+    constexpr int STAGE = BM * (BN + 8);             // epilogue staging (bf16 elements, padded rows)
     constexpr int LDSN = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
     __shared__ __attribute__((aligned(16))) bf16_t lds[LDSN];
     bf16_t* As = lds;                                // [2][BM][LDS_ROW]
@@ -1424,22 +1511,51 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         }
         return;
     }
+    {
+        // general tile (wide outputs: DGRAD of a merged Dense, FWD with N > BN): the tile is staged in LDS
+        // and leaves as row segments of 8 columns -- 16-, 8- or 4-byte stores by the segment's alignment
+        // (row stride N need not be a multiple of 8) -- instead of the MFMA layout's 2-byte column stores
+        constexpr int SROW = BN + 8;
+        bf16_t* st = lds;                            // k loop done (last barrier above)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-        const int col = n0 + wc * (BN / 2) + j * 16 + r16;
-        if (col >= N) continue;
-        const float bv = bias ? bias[col] : 0.f;
+        for (int j = 0; j < NTW; ++j) {
+            const int cl = wc * (BN / 2) + j * 16 + r16;
+            const float bv = (bias && n0 + cl < N) ? bias[n0 + cl] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = m0 + wr * 64 + i * 16 + rq + r;
-                if (row >= M) continue;
-                const int64_t off = (int64_t)row * N + col;
-                float v = apply_act(acc[i][j][r] + bv, oact);
-                if (accum) v += bf2f(o[off]);
-                o[off] = f2bf(v);
+                for (int r = 0; r < 4; ++r)
+                    st[(wr * 64 + i * 16 + rq + r) * SROW + cl] = f2bf(apply_act(acc[i][j][r] + bv, oact));
+        }
+        __syncthreads();
+        const int nrows = min(BM, M - m0), ncols = min(BN, N - n0);
+        constexpr int CH = BN / 8;
+        for (int u = t; u < BM * CH; u += 256) {
+            const int r = u / CH, c8 = (u % CH) * 8;
+            if (r >= nrows || c8 >= ncols) continue;
+            const int64_t g = (int64_t)(m0 + r) * N + n0 + c8;
+            Frag f;
+            f.u = *reinterpret_cast<const uint4*>(&st[r * SROW + c8]);
+            const int nv = min(8, ncols - c8);
+            if (accum) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (e < nv) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(o[g + e]));
             }
+            if (nv == 8 && (g & 7) == 0) {
+                *reinterpret_cast<uint4*>(o + g) = f.u;
+            } else if (nv == 8 && (g & 3) == 0) {
+                *reinterpret_cast<uint2*>(o + g) = make_uint2(f.w[0], f.w[1]);
+                *reinterpret_cast<uint2*>(o + g + 4) = make_uint2(f.w[2], f.w[3]);
+            } else if (nv == 8 && (g & 1) == 0) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) *reinterpret_cast<uint32_t*>(o + g + 2 * w) = f.w[w];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (e < nv) o[g + e] = f.h[e];
+            }
+        }
     }
 }
 
@@ -1451,7 +1567,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
 // variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
-//                 narrow (K <= 4): 4000000 + K; tiles (prob, row block, 0, 0)
+//                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, F % 8 != 0); tiles (prob, row block, 0, 0)
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
 //                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
@@ -1461,11 +1577,12 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     const int4* tp = as_ptr<const int4>(tiles);
     dim3 grid((unsigned)ntiles), block(256);
     if (mode == MODE_WGRAD && variant >= 4000000) {
-        const int k = variant - 4000000;
-        if (k == 1) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<1>), grid, block, 0, s, dp, tp);
-        else if (k == 2) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<2>), grid, block, 0, s, dp, tp);
-        else if (k == 3) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<3>), grid, block, 0, s, dp, tp);
-        else if (k == 4) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<4>), grid, block, 0, s, dp, tp);
+        const int k = (variant - 4000000) % 100;
+        const bool st = (variant - 4000000) >= 100;
+#define NW(K_) if (k == K_) { if (st) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<K_, true>), grid, block, 0, s, dp, tp); \
+                              else hipLaunchKernelGGL((g3_narrow_wgrad_kernel<K_, false>), grid, block, 0, s, dp, tp); }
+        NW(1) else NW(2) else NW(3) else NW(4)
+#undef NW
         else throw std::runtime_error("gemm3: unknown narrow WGRAD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
         return;
@@ -1526,11 +1643,12 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         return;
     }
     if (mode == MODE_FWD && variant >= 6000 && variant < 7000) {
-        const int k = variant - 6000;
-        if (k == 1) hipLaunchKernelGGL((g3_narrow_fwd_kernel<1>), grid, block, 0, s, dp, tp);
-        else if (k == 2) hipLaunchKernelGGL((g3_narrow_fwd_kernel<2>), grid, block, 0, s, dp, tp);
-        else if (k == 3) hipLaunchKernelGGL((g3_narrow_fwd_kernel<3>), grid, block, 0, s, dp, tp);
-        else if (k == 4) hipLaunchKernelGGL((g3_narrow_fwd_kernel<4>), grid, block, 0, s, dp, tp);
+        const int k = (variant - 6000) % 100;
+        const bool st = (variant - 6000) >= 100;
+#define NF(K_) if (k == K_) { if (st) hipLaunchKernelGGL((g3_narrow_fwd_kernel<K_, true>), grid, block, 0, s, dp, tp); \
+                              else hipLaunchKernelGGL((g3_narrow_fwd_kernel<K_, false>), grid, block, 0, s, dp, tp); }
+        NF(1) else NF(2) else NF(3) else NF(4)
+#undef NF
         else throw std::runtime_error("gemm3: unknown narrow FWD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
         return;
