@@ -471,7 +471,7 @@ class HipPopulationEngine(PopulationEngine):
         k = max(1, min(int(nstreams), P))
         if k == 1:
             return [list(range(P))]
-        costs = [float(lay.ir.flops_per_sample()) + 1.0 for lay in self.layouts]
+        costs = [float(lay.ir.cost_per_sample()) + 1.0 for lay in self.layouts]
         order = sorted(range(P), key=lambda o: -costs[o])
         loads = [0.0] * k
         groups: List[List[int]] = [[] for _ in range(k)]

@@ -52,6 +52,6 @@ def plan_generation(sources: Sequence[str], cache: InterpretCache, max_parameter
     with np.errstate(invalid="ignore"):
         is_overweight = params > max_parameters          # NaN > x is False, as in the reference
     trainable = np.nonzero(is_valid & ~is_overweight)[0]
-    costs = np.array([3.0 * results[i].ir.flops_per_sample() + 1e5 for i in trainable], dtype=np.float64)
+    costs = np.array([results[i].ir.cost_per_sample() + 1e5 for i in trainable], dtype=np.float64)
     keys = [results[i].ir.arch_hash() for i in trainable]
     return GenerationPlan(results, is_valid, is_overweight, trainable, costs, keys)

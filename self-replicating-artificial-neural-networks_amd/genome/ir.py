@@ -18,6 +18,7 @@ can batch heterogeneous organisms into grouped kernels:
 from __future__ import annotations
 
 import hashlib
+import os
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -109,6 +110,24 @@ class OrganismIR:
 
     def flops_per_sample(self) -> float:
         return sum(n.flops_per_sample() for n in self.nodes)
+
+    def cost_per_sample(self) -> float:
+        """Estimated training time per sample (arbitrary units) of this organism on the HIP engine: per
+        node the larger of its MFMA time and its memory time (a roofline with the rates the grouped
+        kernels reach on small layers, measured: ~100 TFLOP/s, ~1.5 TB/s), summed over forward +
+        backward (3x the forward FLOPs; ~6 passes over each node's input and output, bf16).  Used to
+        balance organisms across ranks and HIP streams: FLOPs alone under-weight the memory-bound
+        layers (BatchNormalization, Dense on 75,000-row inputs) that dominate many organisms."""
+        if os.environ.get("SERANN_COST", "time") == "flops":
+            return 3.0 * self.flops_per_sample()
+        by_id = {n.id: n for n in self.nodes}
+        t = 0.0
+        for n in self.nodes:
+            if n.op in ("input", "reshape"):
+                continue
+            elems = float(math.prod(n.shape)) + sum(float(math.prod(by_id[i].shape)) for i in n.inputs)
+            t += max(3.0 * n.flops_per_sample() / 100e12, 6.0 * 2.0 * elems / 1.5e12)
+        return t * 1e12
 
     def activation_elems_per_sample(self) -> int:
         return sum(math.prod(n.shape) for n in self.nodes if n.op not in ("reshape", "input"))
