@@ -1070,7 +1070,10 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     const int RPI = 256 / FC;
     const int t = threadIdx.x;
     const bool active = t < RPI * FC;
-    if (!ST && !active) return;
+    // GF_BNSTAT: this output feeds a BatchNormalization -- accumulate its phase-0 statistics here
+    // (shifted sums against row 0's value, exactly what bn phase 0 would read) into aux[c], aux[N + c]
+    const bool bnstat = (d.flags & GF_BNSTAT) != 0;
+    if (!ST && !bnstat && !active) return;
     const int chunk = t % FC, rl = t / FC;
     const int f0 = chunk * 8;
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.a);
@@ -1085,6 +1088,25 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
 #pragma unroll
         for (int k = 0; k < K; ++k) w[j][k] = bf2f(Wm[f * K + k]);
     }
+    float ks[8], s1[8], s2[8];                   // BN shift (row 0's output) and partial sums
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ks[j] = 0.f; s1[j] = 0.f; s2[j] = 0.f; }
+    if (bnstat) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float v = bv[j];
+#pragma unroll
+            for (int k = 0; k < K; ++k) v += bf2f(X[k]) * w[j][k];
+            ks[j] = bf2f(f2bf(apply_act(v, act)));
+        }
+    }
+    auto stat = [&](int j, bf16_t o) {
+        if (bnstat) {
+            const float dv = bf2f(o) - ks[j];
+            s1[j] += dv;
+            s2[j] += dv * dv;
+        }
+    };
     const bool vec = (N & 7) == 0;
     const int r0 = td.y * NARROW_ROWS, r1 = min(M, r0 + NARROW_ROWS);
     constexpr int U = 4;                         // rows in flight per thread
@@ -1111,7 +1133,9 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                             float v = bv[j];
 #pragma unroll
                             for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
-                            st[(r - p0) * N + f0 + j] = f2bf(apply_act(v, act));
+                            const bf16_t o = f2bf(apply_act(v, act));
+                            stat(j, o);
+                            st[(r - p0) * N + f0 + j] = o;
                         }
                     }
                 }
@@ -1125,36 +1149,60 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
             for (int e = nvec * 8 + t; e < total; e += 256) dst[e] = st[e];
             __syncthreads();
         }
-        return;
-    }
-    for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
-        float xv[U][K];
+    } else if (active) {
+        for (int rb = r0 + rl; rb < r1; rb += U * RPI) {
+            float xv[U][K];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = min(rb + u * RPI, r1 - 1);
+            for (int u = 0; u < U; ++u) {
+                const int r = min(rb + u * RPI, r1 - 1);
 #pragma unroll
-            for (int k = 0; k < K; ++k) xv[u][k] = bf2f(X[(int64_t)r * ldx + k]);
+                for (int k = 0; k < K; ++k) xv[u][k] = bf2f(X[(int64_t)r * ldx + k]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = rb + u * RPI;
+                if (r >= r1) break;
+                union { uint4 u4; bf16_t h[8]; } o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float v = bv[j];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
+                    o.h[j] = f2bf(apply_act(v, act));
+                    if (f0 + j < N) stat(j, o.h[j]);
+                }
+                bf16_t* dst = Y + (int64_t)r * N + f0;
+                if (vec) {
+                    *reinterpret_cast<uint4*>(dst) = o.u4;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (f0 + j < N) dst[j] = o.h[j];
+                }
+            }
         }
+    }
+    if (bnstat) {
+        // combine the RPI row lanes of every (chunk, channel) through LDS; one atomic pair per channel
+        __shared__ float red[2 * 8 * 256];
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = rb + u * RPI;
-            if (r >= r1) break;
-            union { uint4 u4; bf16_t h[8]; } o;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                float v = bv[j];
-#pragma unroll
-                for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
-                o.h[j] = f2bf(apply_act(v, act));
+        for (int j = 0; j < 8; ++j) {
+            red[j * 256 + t] = active ? s1[j] : 0.f;
+            red[(8 + j) * 256 + t] = active ? s2[j] : 0.f;
+        }
+        __syncthreads();
+        float* ws = reinterpret_cast<float*>(d.aux);
+        for (int o = t; o < FC * 8; o += 256) {
+            const int ch = o >> 3, j = o & 7, c = ch * 8 + j;
+            if (c >= N) continue;
+            float a = 0.f, b = 0.f;
+            for (int q = 0; q < RPI; ++q) {
+                a += red[j * 256 + q * FC + ch];
+                b += red[(8 + j) * 256 + q * FC + ch];
             }
-            bf16_t* dst = Y + (int64_t)r * N + f0;
-            if (vec) {
-                *reinterpret_cast<uint4*>(dst) = o.u4;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (f0 + j < N) dst[j] = o.h[j];
-            }
+            atomicAdd(ws + c, a);
+            atomicAdd(ws + N + c, b);
         }
     }
 }

@@ -28,6 +28,8 @@ enum GemmFlags : int64_t {
     GF_SPLITWS = 64,      // FWD (LDS-tiled kernel): k range split over blocks; each split stores its raw
                           // fp32 partial tile to the workspace aux[split][M][N]; splitk_finalize sums
                           // the splits and applies bias + activation (no atomics, no zeroing)
+    GF_BNSTAT = 128,      // FWD narrow kernel: also accumulate the consuming BatchNorm's phase-0 statistics
+                          // into aux (shifted sums, aux[c] and aux[N + c])
     GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
                           // into a zeroed output, the bias added by the split that starts at k = 0
 };

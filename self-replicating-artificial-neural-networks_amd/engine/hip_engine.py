@@ -39,6 +39,7 @@ ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp
 SLACK = 64  # elements of zeroed tail on every arena
 # v3 (default): buffer-load direct-fragment FWD/DGRAD with magic-number im2col + 64-row WGRAD;
 # v2: first direct-fragment version; v1: LDS-tiled version.  Kept selectable for A/B measurements.
+FUSE_BN_STATS = os.environ.get("SERANN_FUSE_BN_STATS", "1") != "0"
 GEMM_IMPL = os.environ.get("SERANN_GEMM", "v3")
 
 
@@ -626,6 +627,17 @@ class HipPopulationEngine(PopulationEngine):
         plan.imcol_lookup = raw_conv_imcol
 
         fcat, fcons = self._fused_concats(mem, org_iter)
+        # gemm node -> the (first) last-axis BatchNormalization reading its output with matching channels
+        bn_consumer = [dict() for _ in range(P)]
+        bn_prefused = set()
+        for o, lay in org_iter():
+            owner = mem["orgs"][o]["owner"]
+            for n in lay.ir.nodes:
+                if n.op == "bn" and n.attrs["last"]:
+                    src = lay.ir.node(owner[n.inputs[0]])
+                    if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
+                            and src.attrs["f"] == n.attrs["channels"] and src.id not in bn_consumer[o]):
+                        bn_consumer[o][src.id] = n.id
 
         def concat_slices(o, n, F):
             """K slices (input node, first column, width, k splits, first workspace slot) of a fused-concat
@@ -643,7 +655,7 @@ class HipPopulationEngine(PopulationEngine):
             fin_rows = []
             g_rows, g_dims = [], []
             p_rows, p_cnt = [], []
-            bn_rows, bn_cnt, bn_cnt_st = [], [], []
+            bn_rows, bn_cnt, bn_cnt_st, bn_stat = [], [], [], []
             c_rows, c_cnt = [], []
             fallbacks = []
             for o, lay in org_iter():
@@ -700,6 +712,14 @@ class HipPopulationEngine(PopulationEngine):
                             g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
                                                OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
                                                flags=flags))
+                            # a narrow-kernel output that feeds a BatchNormalization: the BN statistics
+                            # (phase 0) are accumulated by the producing kernel itself
+                            bnc = bn_consumer[o].get(n.id)
+                            if (train and bnc is not None and FUSE_BN_STATS
+                                    and H.narrow_k(g_rows[-1], H.MODE_FWD, M, F, K) is not None):
+                                g_rows[-1]["aux"] = mem["ws"].ptr(rec["bn"][bnc]["ws"])
+                                g_rows[-1]["flags"] |= H.GF_BNSTAT
+                                bn_prefused.add((o, bnc))
                         if n.id not in fcons[o]:
                             g_dims.append((M, F, K))      # (K slices appended their own dims)
                     elif n.op == "pool":
@@ -722,6 +742,7 @@ class HipPopulationEngine(PopulationEngine):
                                             flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
                         bn_cnt.append(H.bn_chunks(B * math.prod(n.shape) // c, c))
                         bn_cnt_st.append(H.bn_chunks(B * math.prod(n.shape) // c, c, stats=True))
+                        bn_stat.append((o, n.id) not in bn_prefused)
                     elif n.op == "concat":
                         if n.id in fcat[o]:
                             continue                  # read in place by its consumers' K slices
@@ -743,7 +764,8 @@ class HipPopulationEngine(PopulationEngine):
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             if bn_rows:
                 if train:
-                    add_chunked("bn", 0, bn_rows, H.BN_DTYPE, bn_cnt_st, 1)
+                    need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)
+                    add_chunked("bn", 0, [bn_rows[i] for i in need0], H.BN_DTYPE, [bn_cnt_st[i] for i in need0], 1)
                     add_chunked("bn", 2, bn_rows, H.BN_DTYPE, bn_cnt, 1)
                 else:
                     add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, 1)

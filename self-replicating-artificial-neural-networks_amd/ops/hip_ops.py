@@ -32,7 +32,7 @@ SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kern
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
-GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS = 1, 2, 4, 8, 16, 32, 64
+GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 32, 64, 128
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 

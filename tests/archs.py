@@ -1,6 +1,21 @@
 """Architecture corpus for engine/kernel parity tests (decoded, no-space form and template form)."""
 
 ARCHS = {
+    # the example.json ancestor's shape (table codec): narrow Dense on the raw genotype feeding a
+    # BatchNormalization (fused BN statistics), concat with the raw image (fused concat, no DGRAD slice)
+    "narrow_bn_ancestor": (
+        "g_layer = Dense(units=75, activation='relu')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=152, activation='relu')(con)\n\nloss_balance = 0.85"),
+    # (relu, not sigmoid: a BN right after a sigmoid of the raw image normalises outputs whose spread is
+    # ~0.05, where bf16 storage (2^-9 near 0.5) alone is a ~4 % error -- an ill-conditioned parity case)
+    "narrow_bn_x": (
+        "X_layer = Dense(units=24, activation='relu')(X_layer)\n"
+        "X_layer = BatchNormalization()(X_layer)\n\n"
+        "g_layer = Dense(units=16, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=40, activation='relu')(con)\n\nloss_balance = 0.4"),
     "conv_pool_dense": (
         "X_layer = Conv2D(filters=16, kernel_size=5, strides=1)(X_layer)\n"
         "X_layer = MaxPool2D(pool_size=2)(X_layer)\n"
