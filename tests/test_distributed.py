@@ -1,4 +1,4 @@
-"""Multi-process SPMD on CPU (gloo, world_size 2): the sharded run must write exactly the same
+"""Multi-process SPMD on CPU (gloo, world_size 2 and 4): the sharded run must write exactly the same
 experiment DB as the single-process run (partition-independent organism seeds, shared batch
 permutation, replicated control plane, one packed all-gather per generation)."""
 import os
@@ -51,13 +51,14 @@ def _read(path):
     return pd.read_sql(f"select {cols} from serann order by generation, id", con)
 
 
-def test_gloo_world2_matches_world1(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_world_matches_world1(tmp_path, world):
     p1 = str(tmp_path / "w1.sqlite")
     _worker(0, 1, _free_port(), p1)
-    p2 = str(tmp_path / "w2.sqlite")
+    p2 = str(tmp_path / f"w{world}.sqlite")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, p2)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, p2)) for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
