@@ -46,4 +46,6 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("imcol", &launch_imcol);
     m.def("embed_gather", &launch_embed_gather);
     m.def("splitk_finalize", &launch_splitk_finalize);
+    m.def("cat_loglik_fwd", &launch_cat_loglik_fwd);
+    m.def("cat_loglik_bwd", &launch_cat_loglik_bwd);
 }

@@ -58,6 +58,9 @@ void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t s
 void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
 void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream);
+void launch_cat_loglik_bwd(uint64_t z, uint64_t x, uint64_t gout, uint64_t dz, int64_t B, int64_t L, int64_t V,
+                           uint64_t stream);
 void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t rows, int64_t E, int64_t V,
                          uint64_t stream);

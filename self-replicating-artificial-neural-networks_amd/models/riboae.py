@@ -20,6 +20,7 @@ does the encode path (embedding gather, LDS-halo convolutions, split-K Dense, gr
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -99,12 +100,14 @@ class GenerativeNet(nn.Module):
         _glorot_(self.dense.weight, self.flat, max_len * vocab)
         nn.init.zeros_(self.dense.bias)
 
-    def forward(self, z):                                          # z: (B, G, A)
+    def logits(self, z):                                           # pre-softmax (B, L, V)
         x = self.conv(z.permute(0, 2, 1))                          # (B, 32, G-4)
         x = self.bn1(x.permute(0, 2, 1))                           # (B, G-4, 32)
         x = self.dense(x.reshape(x.shape[0], -1))
-        x = self.bn2(x.view(-1, self.max_len, self.vocab))
-        return F.log_softmax(x, dim=-1)
+        return self.bn2(x.view(-1, self.max_len, self.vocab))
+
+    def forward(self, z):                                          # z: (B, G, A)
+        return F.log_softmax(self.logits(z), dim=-1)
 
 
 class GeneticAutoencoder(nn.Module):
@@ -130,6 +133,11 @@ class GeneticAutoencoder(nn.Module):
         return logits.argmax(-1)
 
     def _decode(self, x, z):
+        if z.is_cuda and os.environ.get("SERANN_RIBOAE_HIP", "1") != "0":
+            from ..ops.riboae_ops import available, categorical_loglik
+            if available():
+                # fused log-softmax + gather + sum over the sequence (HIP)
+                return categorical_loglik(self.generative_net.logits(z), x)
         logp = self.generative_net(z)                               # (B, L, V) log-probs
         return torch.gather(logp, -1, x.long().unsqueeze(-1)).squeeze(-1).sum(-1)
 

@@ -5,6 +5,9 @@ evolutionary_experiment/logic/ribosomal_autoencoder.py:116-124).
   the preceding Conv1D / Dense weights, so decode is two grouped MFMA GEMM launches (Conv1D 2->32 k5 as
   an implicit-GEMM conv; Dense 3072 -> 350*V with fp32 output) and one fused group-argmax launch.
   log_softmax is monotone, so it is never materialised.
+* Training (K37): ``categorical_loglik`` -- log-softmax over the vocabulary, gather at the target
+  tokens and the sum over the sequence in one HIP kernel (and its backward), instead of materialising
+  the [B][L][V] log-probabilities (model.py:45-46, 54-59).
 * Encode (K30-K32, K35): token ids -> genotype bits.  The one-channel BatchNormalization after the
   embedding is folded into the embedding table, the BatchNormalizations after the three Conv2Ds into
   their weights and biases.  Encode is an embedding-gather launch, three LDS-halo MFMA convolutions
@@ -202,3 +205,29 @@ class HipRiboEncoder:
                 lib.group_argmax(pl["logits"].data_ptr(), pl["bits"].data_ptr(), B * self.G, self.A, s)
                 outs.append(pl["bits"].view(B, self.G).long().clone())
         return torch.cat(outs, 0)
+
+
+class _CatLogLik(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, x):
+        z = z.float().contiguous()
+        x = x.to(torch.int64).contiguous()
+        B, L, V = z.shape
+        out = torch.zeros(B, dtype=torch.float32, device=z.device)
+        H.lib().cat_loglik_fwd(z.data_ptr(), x.data_ptr(), out.data_ptr(), B, L, V, H.stream_handle())
+        ctx.save_for_backward(z, x)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        z, x = ctx.saved_tensors
+        B, L, V = z.shape
+        dz = torch.empty_like(z)
+        H.lib().cat_loglik_bwd(z.data_ptr(), x.data_ptr(), g.float().contiguous().data_ptr(), dz.data_ptr(), B, L, V,
+                               H.stream_handle())
+        return dz, None
+
+
+def categorical_loglik(z: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """sum_l log_softmax(z[b, l])[x[b, l]] -> (B,) on the HIP kernels (z: [B][L][V] pre-softmax)."""
+    return _CatLogLik.apply(z, x)
