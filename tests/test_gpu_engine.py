@@ -94,7 +94,9 @@ def test_population_grouping_matches_single():
             for k in b[nid]:
                 if k.startswith("moving"):
                     continue
-                assert _rel(a[nid][k], b[nid][k]) < 5e-2 or np.linalg.norm(b[nid][k]) < 1e-3, (names[i], nid, k)
+                # (gradients that are mathematically ~0 -- the bias of a layer feeding BatchNormalization --
+                # are float-atomic-order noise of ~1e-3 in either engine: absolute check)
+                assert _rel(a[nid][k], b[nid][k]) < 5e-2 or np.linalg.norm(b[nid][k]) < 5e-3, (names[i], nid, k)
 
 
 def test_fit_graph_replay_learns():
