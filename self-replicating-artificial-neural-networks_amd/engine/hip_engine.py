@@ -545,7 +545,7 @@ class HipPopulationEngine(PopulationEngine):
                     for r in rws:
                         ns = int(r.pop("_split", 1))
                         if ns > 1 and not r.get("_pre"):
-                            wsb = torch.empty(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
+                            wsb = torch.zeros(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
                             plan.keep.append(wsb)
                             r["aux"] = wsb.data_ptr()
                             fin.append(dict(ws=r["aux"], out=r["out"], bias=r.get("bias", 0), M=r["M"], N=r["N"],
@@ -693,7 +693,7 @@ class HipPopulationEngine(PopulationEngine):
                             # (no concat copy); fp32 partials + one finalize (bias, activation)
                             D = ir.head_features if a["kind"] == "head_cls" else C
                             sl, S = concat_slices(o, n, F)
-                            wsb = torch.empty(S * M * F, dtype=torch.float32, device=self.device)
+                            wsb = torch.zeros(S * M * F, dtype=torch.float32, device=self.device)
                             plan.keep.append(wsb)
                             for pid, col, width, ns, sb in sl:
                                 g_rows.append(dict(a=self._act_ptr(mem, o, pid, inputs), b=wptr_bf(lay.w[n.id]) + 2 * col,
