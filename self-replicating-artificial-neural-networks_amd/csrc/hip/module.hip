@@ -46,6 +46,8 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("imcol", &launch_imcol);
     m.def("embed_gather", &launch_embed_gather);
     m.def("splitk_finalize", &launch_splitk_finalize);
+    m.def("concrete_fwd", &launch_concrete_fwd);
+    m.def("concrete_bwd", &launch_concrete_bwd);
     m.def("cat_loglik_fwd", &launch_cat_loglik_fwd);
     m.def("cat_loglik_bwd", &launch_cat_loglik_bwd);
 }

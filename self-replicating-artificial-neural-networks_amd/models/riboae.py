@@ -182,19 +182,28 @@ class ConcreteGAE(GeneticAutoencoder):
         self.prior_temperature = prior_temperature
         self.hparams["prior_temperature"] = prior_temperature
 
-    def _encode(self, x, temperature=0.2):
+    def _encode(self, x, temperature=0.2, noise=None):
         logits = self.inference_net(x)
         loc = logits / temperature
         scale = 1.0 / temperature
-        u = torch.rand_like(loc).clamp_(1e-20, 1 - 1e-7)
+        u = (torch.rand_like(loc) if noise is None else noise.to(loc)).clamp(1e-20, 1 - 1e-7)
         sample = loc - scale * torch.log(-torch.log(u))            # Gumbel(loc, scale) sample
         logq = gumbel_log_prob(sample, loc, scale)
         ploc = math.log(1.0 / self.alphabet) / self.prior_temperature
         logp = gumbel_log_prob(sample, ploc, 1.0 / self.prior_temperature)
         return torch.softmax(sample, -1), logq, logp
 
-    def compute_loss(self, x, temperature, kld_weight) -> Dict[str, torch.Tensor]:
-        z, logq, logp = self._encode(x, temperature)
+    def compute_loss(self, x, temperature, kld_weight, noise=None) -> Dict[str, torch.Tensor]:
+        """NELBO (model.py:88-100).  ``noise``: optional uniforms of the logits' shape (B, G, A) replacing
+        the random draw, so two runs (or the HIP and the torch path) see the same sample."""
+        if x.is_cuda and os.environ.get("SERANN_RIBOAE_HIP", "1") != "0":
+            from ..ops.riboae_ops import available, concrete_sample
+            if available():                                        # K36 fused sample + softmax + KL
+                z, kl = concrete_sample(self.inference_net(x), temperature, self.prior_temperature, noise)
+                logpx_z = self._decode(x, z)
+                nelbo = -(logpx_z - kld_weight * kl).mean()
+                return {"loss": nelbo, "nll": -logpx_z.mean(), "kld": kl.mean()}
+        z, logq, logp = self._encode(x, temperature, noise)
         logpx_z = self._decode(x, z)
         kl = (logq - logp).flatten(1).sum(1)
         nelbo = -(logpx_z - kld_weight * kl).mean()

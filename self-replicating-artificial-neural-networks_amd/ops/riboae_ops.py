@@ -207,6 +207,47 @@ class HipRiboEncoder:
         return torch.cat(outs, 0)
 
 
+class _Concrete(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, t, tp, u):
+        logits = logits.float().contiguous()
+        B, G, A = logits.shape
+        s = torch.empty_like(logits)
+        z = torch.empty_like(logits)
+        kl = torch.zeros(B, dtype=torch.float32, device=logits.device)
+        if u is None:
+            # Philox key/offset drawn from torch's CPU generator: torch.manual_seed reproduces the sample
+            seed, off = (int(v) for v in torch.randint(0, 2 ** 31 - 1, (2,)))
+            seed = (seed << 31) | int(torch.randint(0, 2 ** 31 - 1, (1,)))
+            uptr = 0
+        else:
+            u = u.float().contiguous()
+            uptr, seed, off = u.data_ptr(), 0, 0
+        H.lib().concrete_fwd(logits.data_ptr(), uptr, s.data_ptr(), z.data_ptr(), kl.data_ptr(), B, G, A, float(t),
+                             float(tp), seed, off, H.stream_handle())
+        ctx.save_for_backward(s, z)
+        ctx.t, ctx.tp = float(t), float(tp)
+        return z, kl
+
+    @staticmethod
+    def backward(ctx, gz, gkl):
+        s, z = ctx.saved_tensors
+        B, G, A = s.shape
+        d = torch.empty_like(s)
+        gz = gz.float().contiguous() if gz is not None else None
+        gkl = gkl.float().contiguous() if gkl is not None else None
+        H.lib().concrete_bwd(s.data_ptr(), z.data_ptr(), gz.data_ptr() if gz is not None else 0,
+                             gkl.data_ptr() if gkl is not None else 0, d.data_ptr(), B, G, A, ctx.t, ctx.tp,
+                             H.stream_handle())
+        return d, None, None, None
+
+
+def concrete_sample(logits: torch.Tensor, temperature: float, prior_temperature: float, u=None):
+    """K36: (softmax of a Gumbel(logits/t, 1/t) sample, per-row KL sum_{g,a} log q - log p) on the HIP
+    kernels; ``u`` (same shape as logits) replaces the in-kernel Philox uniforms when given."""
+    return _Concrete.apply(logits, temperature, prior_temperature, u)
+
+
 class _CatLogLik(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, x):
