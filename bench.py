@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--pop-per-gpu", type=int, default=125)
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--parameters", default=None)
-    ap.add_argument("--profile-dir", default=None)
+    ap.add_argument("--profile-dir", default=None,
+                    help="torch.profiler Chrome trace of the run per rank (diagnostics; not a headline timing)")
     args = ap.parse_args()
 
     import numpy as np
@@ -78,7 +79,9 @@ def main():
     if args.warmup == 0:
         comm.barrier()
         marks["t0"] = time.perf_counter()
-    hist = exp.execute(on_generation=on_generation)
+    from serann.utils.trace import profiled
+    with profiled(args.profile_dir, f"rank{comm.rank}"):
+        hist = exp.execute(on_generation=on_generation)
     if is_cuda:
         torch.cuda.synchronize()
     comm.barrier()

@@ -34,8 +34,10 @@ import pandas as pd
 from ..genome.interpreter import layer_counts
 from ..parallel.comm import Comm, LocalComm, pack_results, unpack_results
 from ..parallel.partition import lpt_partition
+from ..utils.faults import maybe_inject
 from ..utils.levenshtein import levenshtein_batch
 from ..utils.stats import fertility, genotype_stats, source_code_stats
+from ..utils.trace import PhaseTimer, phase
 from .population import InterpretCache, plan_generation
 from .worker import ShardWorker
 
@@ -95,13 +97,16 @@ class Experiment:
             generation_start_time = datetime.now()
             t0 = time.perf_counter()
             self.log(f"### Generation {generation_number} execution has started ###")
+            maybe_inject(generation_number, self._comm.rank)          # SERANN_FAULT_INJECT (recovery tests)
+            timer = PhaseTimer()
             current["experiment_id"] = self._id
             current["generation"] = generation_number
             current["num_offspring"] = 0
 
             self.log("Starting training and replication")
-            models_info, offspring_by_id, times = self._learn_and_replicate(current, offspring_pool_size,
-                                                                           generation_number)
+            with phase("learn_and_replicate", timer):
+                models_info, offspring_by_id, times = self._learn_and_replicate(current, offspring_pool_size,
+                                                                               generation_number)
             current = current.join(models_info)
 
             self.log("Calculating fecundity scores")
@@ -120,12 +125,15 @@ class Experiment:
             current = current.join(stats, how="left")
 
             t_stats = time.perf_counter()
-            generation_info = self._generation_statistics(current, generation_number, times, generation_start_time)
+            with phase("statistics", timer):
+                generation_info = self._generation_statistics(current, generation_number, times,
+                                                              generation_start_time)
             if self._comm.is_root and self._db is not None:
-                self.log("Saving generation information to the experiment DB")
-                self._db.save_generation_info(generation_info)
-                self.log("Saving SeRANN records to the experiment DB")
-                self._db.save_seranns_info(current)
+                with phase("db_write", timer):
+                    self.log("Saving generation information to the experiment DB")
+                    self._db.save_generation_info(generation_info)
+                    self.log("Saving SeRANN records to the experiment DB")
+                    self._db.save_seranns_info(current)
             t_db = time.perf_counter()
 
             record = dict(generation=generation_number, seconds=None, learning_time=float(np.mean(times["learning_times"] or [0])),
@@ -142,7 +150,8 @@ class Experiment:
                 break
 
             self.log("Applying offspring selection")
-            next_generation = self._select_offspring(current, offspring_by_id)
+            with phase("selection", timer):
+                next_generation = self._select_offspring(current, offspring_by_id)
             self.log(f"Generation {generation_number} execution is done")
             offspring_pool_size = int(current["num_offspring"].max() * p["offspring_pool_size_factor"])
             self.log("Offspring pool size was updated to:", offspring_pool_size)
@@ -152,6 +161,7 @@ class Experiment:
                     "rng": self._rng.get_state()})
             current = next_generation
             record["seconds"] = time.perf_counter() - t0
+            record["phases"] = timer.reset()
             self._print_generation_time(record["seconds"])
             self._finish_record(record, on_generation)
         return self.history

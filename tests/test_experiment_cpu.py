@@ -76,3 +76,50 @@ def test_multi_generation_determinism(tmp_path, small_data):
     later = pd.read_sql("select * from serann where generation > 0", sqlite3.connect(db1.db_path))
     assert later["parent_id"].notna().all()
     assert later["genotype"].iloc[0].startswith("[0.0") or later["genotype"].iloc[0].startswith("[1.0")
+
+
+def test_injected_fault_then_exact_resume(tmp_path, small_data, monkeypatch):
+    """a rank dies at generation 2 (SERANN_FAULT_INJECT); relaunching from the DB
+    (start generation = rows in ``generations``, as ``--resume-experiment-id`` does) continues from
+    ``resume_state`` and writes exactly the rows of an uninterrupted run."""
+    from serann.utils.faults import InjectedFault
+    ref_db, _ = _run(tmp_path, small_data, pop=4, gens=4, name="ref.sqlite")
+
+    enc, data = small_data
+    p = default_parameters("example")
+    p.update(num_seranns=4, num_generations=4, training_epochs=1)
+    codec = TableCodec.from_generator(128, seed=1, ancestor=p["ancestor_genotype"])
+
+    def experiment(db, start):
+        w = ShardWorker(p, data, "torch", "cpu", TrainConfig(epochs=1, batch_size=200))
+        return Experiment("exp", enc, w, db, p, codec, random_seed=5, verbose=False, start_generation=start)
+
+    db = ExperimentDB(tmp_path / "crash.sqlite")
+    monkeypatch.setenv("SERANN_FAULT_INJECT", "generation=2")
+    with pytest.raises(InjectedFault):
+        experiment(db, 0).execute()
+    assert db.get_generations_count() == 2
+    monkeypatch.delenv("SERANN_FAULT_INJECT")
+    hist = experiment(db, db.get_generations_count()).execute()
+    assert [h["generation"] for h in hist] == [2, 3]
+    assert set(hist[0]["phases"]) >= {"learn_and_replicate", "statistics", "db_write", "selection"}
+
+    cols = ("id, genotype, source_code, parent_id, generation, num_offspring, classification_validation_accuracy,"
+            " replication_mse")
+    a = pd.read_sql(f"select {cols} from serann", sqlite3.connect(ref_db.db_path))
+    b = pd.read_sql(f"select {cols} from serann", sqlite3.connect(db.db_path))
+    pd.testing.assert_frame_equal(a, b)
+    info = pd.read_sql("select * from execution_info", sqlite3.connect(db.db_path))
+    assert len(info) == 2                                  # one execution_info row per launch
+
+
+def test_fault_spec_parsing():
+    from serann.utils.faults import InjectedFault, maybe_inject, parse
+    assert parse("generation=3,rank=1,mode=exit") == {"generation": 3, "rank": 1, "mode": "exit"}
+    assert parse("") is None
+    with pytest.raises(ValueError):
+        parse("rank=1")
+    maybe_inject(3, rank=0, spec="generation=3,rank=1")     # other rank: no fault
+    maybe_inject(2, rank=1, spec="generation=3,rank=1")     # other generation: no fault
+    with pytest.raises(InjectedFault):
+        maybe_inject(3, rank=1, spec="generation=3,rank=1")
