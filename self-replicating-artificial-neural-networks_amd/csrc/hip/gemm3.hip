@@ -1058,7 +1058,8 @@ constexpr int NARROW_WROWS = 1024;      // WGRAD rows per block
 // ST (output channels N % 8 != 0, e.g. Dense(units=75) on the raw genotype): the rows are computed
 // into an LDS tile and leave as one contiguous range with 16-B stores -- the row stride N is not a
 // multiple of 8, so per-thread 16-B row chunks are not aligned and the plain path stores 2-B elements.
-constexpr int NARROW_SROWS = 64;        // FWD staged pass (rows): 64 x N (<= 256) bf16 = <= 32 KB
+constexpr int NARROW_SROWS = 64;        // FWD staged pass: 64 x 256 bf16 = 32 KB of LDS, i.e.
+                                        // (64 * 256 / N) & ~7 rows of N channels (<= NARROW_ROWS)
 template <int K, bool ST>
 __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
@@ -1112,8 +1113,11 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     constexpr int U = 4;                         // rows in flight per thread
     if constexpr (ST) {
         __shared__ __attribute__((aligned(16))) bf16_t st[NARROW_SROWS * 256];
-        for (int p0 = r0; p0 < r1; p0 += NARROW_SROWS) {
-            const int p1 = min(r1, p0 + NARROW_SROWS);
+        // rows per pass: fill the buffer (N = 75: 216 rows, 2 passes per block instead of 4); a multiple
+        // of 8 rows keeps every pass's first element 16-B aligned
+        const int srows = min(NARROW_ROWS, ((NARROW_SROWS * 256) / N) & ~7);
+        for (int p0 = r0; p0 < r1; p0 += srows) {
+            const int p1 = min(r1, p0 + srows);
             if (active) {
                 for (int rb = p0 + rl; rb < p1; rb += U * RPI) {
                     float xv[U][K];
@@ -1141,7 +1145,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                 }
             }
             __syncthreads();
-            // rows [p0, p1) are one contiguous range; p0 * N * 2 B is a multiple of 128 B
+            // rows [p0, p1) are one contiguous range; p0 * N * 2 B is a multiple of 16 B
             const int total = (p1 - p0) * N, nvec = total >> 3;
             bf16_t* __restrict__ dst = Y + (int64_t)p0 * N;
             for (int v = t; v < nvec; v += 256)
@@ -1240,10 +1244,13 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
         static_assert(2 * NARROW_WSROWS * 256 * 2 <= 256 * NA * 4, "staging must fit in the reduction array");
         bf16_t* sg = reinterpret_cast<bf16_t*>(red);
         bf16_t* sy = sg + NARROW_WSROWS * 256;
-        for (int p0 = r0; p0 < r1; p0 += NARROW_WSROWS) {
-            const int p1 = min(r1, p0 + NARROW_WSROWS);
+        // rows per pass: fill the 16 x 256 staging buffers (F = 75: 48 rows per pass instead of 16 -- each
+        // pass is one 16-B load per thread between two barriers, so short passes are latency-bound)
+        const int srows = max(8, ((NARROW_WSROWS * 256) / F) & ~7);
+        for (int p0 = r0; p0 < r1; p0 += srows) {
+            const int p1 = min(r1, p0 + srows);
             const int total = (p1 - p0) * F, nvec = total >> 3;
-            // p0 * F * 2 B is a multiple of 32 B: aligned 16-B loads of the contiguous row range
+            // p0 * F * 2 B is a multiple of 16 B: aligned 16-B loads of the contiguous row range
             const bf16_t* gsrc = dY + (int64_t)p0 * F;
             const bf16_t* ysrc = Yv + (int64_t)p0 * F;
             for (int v = t; v < nvec; v += 256) {

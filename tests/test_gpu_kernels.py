@@ -79,6 +79,8 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     (4, 9, 9, 3, 200, 1, 1, 1, 1, "sigmoid"),
     (6, 10, 10, 2, 13, 1, 1, 1, 1, "linear"),
     (30, 100, 1, 1, 75, 1, 1, 1, 1, "relu"),      # narrow + LDS-staged rows (N % 8 != 0): g Dense(75)
+    (30, 100, 1, 2, 37, 1, 1, 1, 1, "sigmoid"),   # staged, K = 2, multi-pass blocks with a ragged tail
+    (13, 100, 1, 1, 130, 1, 1, 1, 1, "relu"),     # staged, N > 128 (several FWD passes per block)
     # wide-f WGRAD tiles (F > 64: one 128- or 256-row f tile per layer)
     (9, 1, 1, 300, 200, 1, 1, 1, 1, "relu"),
     (40, 5, 1, 96, 120, 1, 1, 1, 1, "sigmoid"),
