@@ -4,6 +4,8 @@
                                      and ``parent_*`` columns, cached as a pickle under ``data_cache_dir``;
                                      reads the current ``serann`` table and the legacy ``srann`` table the
                                      reference's loader expects.
+* ``load_experiment_data``        -- the same frame loaded by DB *path*, without ``parent_*`` columns,
+                                     optionally joined with deep-evaluation columns by ``genotype_hex``.
 * ``load_experiment_evaluations`` -- fitness algebra w = V*f*N, W = V*F over deep evaluations.
 * ``load_deep_evaluations``       -- evaluation CSV joined with experiment rows and parents.
 * ``prepare_muller_plot_data``    -- clone identity tracking (IBS) and dominant-clone frames.
@@ -92,6 +94,43 @@ def load_experiment_results(results_name: str, evaluations_name: Optional[str] =
     results = results.join(results.rename(columns={c: f"parent_{c}" for c in results.columns}), on="parent_id")
     results.loc[results["parent_id"].isna(), "parent_genotype_hex"] = "experiment_ancestor_genotype_hex"
     results.loc[results["parent_id"].isna(), "parent_id"] = "experiment_ancestor_id"
+    return results
+
+
+DEEP_EVALUATION_COLUMNS = ["classification_accuracy", "mutation_rate", "offspring_viability", "fecundity",
+                           "normed_fecundity", "fitness"]
+
+
+def load_experiment_data(path: str, deep_evaluations=None, force_download: bool = False,
+                         cache_invalidate: bool = False) -> pd.DataFrame:
+    """Per-organism frame of one experiment DB given by path (reference common/utils.py:199-258).
+
+    Columns: every ``serann`` (or legacy ``srann``) column, ``genotype`` as an int array, ``genotype_hex``,
+    ``is_mutant``, ``descendants`` (transitive descendant count); generation-0 rows get
+    ``parent_id = 'experiment_ancestor_id'`` and ``parent_genotype_hex = 'experiment_ancestor_genotype_hex'``
+    (the reference's boolean-mask assignment of those two raises in pandas; ``.loc`` is what it means).
+    ``deep_evaluations``: a DataFrame or CSV path with ``genotype_hex`` and any of
+    DEEP_EVALUATION_COLUMNS, left-joined on ``genotype_hex`` (first row per genotype).  The frame is
+    cached under ``data_cache_dir`` by DB file name; ``cache_invalidate`` / ``force_download`` rebuild it.
+    """
+    cache_path = Path(config["data_cache_dir"]) / "experiment_data" / (Path(path).name + ".pkl")
+    if not (cache_invalidate or force_download) and cache_path.is_file():
+        with open(cache_path, "rb") as f:       # written by this function (our own file)
+            results = pickle.load(f)
+    else:
+        name = Path(path).stem
+        results = load_experiment_results(name, cache_invalidate=True, db_path=str(path))
+        results = results[[c for c in results.columns if not c.startswith("parent_") or c == "parent_id"]].copy()
+        results["parent_genotype_hex"] = np.where(results["parent_id"] == "experiment_ancestor_id",
+                                                  "experiment_ancestor_genotype_hex", None)
+        cache_path.parent.mkdir(parents=True, exist_ok=True)
+        with open(cache_path, "wb") as f:
+            pickle.dump(results, f)
+    if deep_evaluations is not None:
+        ev = pd.read_csv(deep_evaluations) if isinstance(deep_evaluations, (str, os.PathLike)) else deep_evaluations
+        cols = [c for c in DEEP_EVALUATION_COLUMNS if c in ev.columns]
+        results = results.join(ev[cols + ["genotype_hex"]].drop_duplicates(subset=["genotype_hex"])
+                               .set_index("genotype_hex"), on="genotype_hex", how="left")
     return results
 
 

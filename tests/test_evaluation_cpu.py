@@ -92,3 +92,22 @@ def test_muller_plot_data(experiment):
     pops, adj = prepare_muller_plot_data(df, frequency_threshold=0.0)
     assert {"Generation", "Identity", "Population"} <= set(pops.columns)
     assert (pops.groupby("Generation")["Population"].sum() == 5).all()
+
+
+def test_load_experiment_data_by_path(experiment):
+    from serann.analysis.results import load_experiment_data
+    df, data, codec, p, tmp = experiment
+    path = str(tmp / "exp.sqlite")
+    d = load_experiment_data(path, cache_invalidate=True)
+    assert len(d) == len(df) and not any(c.startswith("parent_") and c not in ("parent_id", "parent_genotype_hex")
+                                         for c in d.columns)
+    g0 = d[d["generation"] == 0]
+    assert (g0["parent_id"] == "experiment_ancestor_id").all()
+    assert (g0["parent_genotype_hex"] == "experiment_ancestor_genotype_hex").all()
+    assert d["genotype"].iloc[0].dtype.kind == "i" and d["descendants"].ge(0).all()
+    # total descendants of generation 0 = every later organism
+    assert d.loc[g0.index, "descendants"].sum() == (d["generation"] > 0).sum()
+    ev = pd.DataFrame({"genotype_hex": [d["genotype_hex"].iloc[0]], "fitness": [0.5], "mutation_rate": [0.1]})
+    j = load_experiment_data(path, deep_evaluations=ev)          # cached frame + evaluation join
+    assert j.loc[j["genotype_hex"] == ev["genotype_hex"][0], "fitness"].eq(0.5).all()
+    assert j["fitness"].isna().sum() == (j["genotype_hex"] != ev["genotype_hex"][0]).sum()
