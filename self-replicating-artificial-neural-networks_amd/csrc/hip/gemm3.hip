@@ -1340,6 +1340,211 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
     }
 }
 
+// "Super-row" (SR) forms of the narrow kernels for a row width W = N (FWD) or F (WGRAD) that is not a
+// multiple of 8 (W > 8).  The [rows][W] tensor is walked in super-rows of 8 rows = W chunks of 8
+// elements; thread i of a super-row always takes chunk i, so its 8 elements always belong to the same
+// channels (8i + j) mod W and lie in rows ro[j] = (8i + j) / W of the super-row (at most two distinct
+// rows, W > 8).  Every global access is an aligned 16-B vector, there is no LDS staging and no barrier
+// in the row loop, the per-channel weights and partial sums stay in registers, and channels are
+// combined once per block through LDS (slot g * 8W + 8i + j holds channel (8i + j) mod W of super-row
+// group g -- the BatchNorm bn_vec layout).
+constexpr int NARROW_SR_U = 4;          // super-rows in flight per thread
+
+template <int K>
+__global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* __restrict__ descs,
+                                                               const int4* __restrict__ tiles) {
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const int M = (int)d.M, N = (int)d.N, act = (int)d.act;
+    const int ldx = (int)d.C;
+    const int t = threadIdx.x, G = 256 / N, q = t / N, i = t - q * N;
+    const bool active = q < G;
+    const bool bnstat = (d.flags & GF_BNSTAT) != 0;
+    const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.a);
+    const bf16_t* __restrict__ Wm = reinterpret_cast<const bf16_t*>(d.b);
+    const float* bias = reinterpret_cast<const float*>(d.bias);
+    bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(d.out);
+    int ch[8], ro[8];
+    float w[8][K], bv[8], ks[8], s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int e = 8 * i + j;
+        ch[j] = e % N;
+        ro[j] = e / N;
+        bv[j] = bias ? bias[ch[j]] : 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) w[j][k] = bf2f(Wm[ch[j] * K + k]);
+        s1[j] = 0.f;
+        s2[j] = 0.f;
+        ks[j] = 0.f;
+        if (bnstat) {              // BN phase-0 shift: row 0's output (what bn phase 0 would read)
+            float v = bv[j];
+#pragma unroll
+            for (int k = 0; k < K; ++k) v += bf2f(X[k]) * w[j][k];
+            ks[j] = bf2f(f2bf(apply_act(v, act)));
+        }
+    }
+    const int64_t total = (int64_t)M * N;
+    const int r0 = td.y * NARROW_ROWS, r1 = min(M, r0 + NARROW_ROWS);
+    const int sr0 = r0 / 8, sr1 = (r1 + 7) / 8;
+    if (active) {
+        constexpr int U = NARROW_SR_U;
+        for (int sb = sr0 + q; sb < sr1; sb += U * G) {
+            float xa[U][K], xb[U][K];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int sr = min(sb + u * G, sr1 - 1);
+                const int ra = min(M - 1, sr * 8 + ro[0]), rb = min(M - 1, ra + 1);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    xa[u][k] = bf2f(X[(int64_t)ra * ldx + k]);
+                    xb[u][k] = bf2f(X[(int64_t)rb * ldx + k]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int sr = sb + u * G;
+                const int64_t e = (int64_t)sr * 8 * N + 8 * i;
+                const int nv = sr < sr1 ? (int)max((int64_t)0, min((int64_t)8, total - e)) : 0;
+                if (nv <= 0) continue;
+                union { uint4 u4; bf16_t h[8]; } o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const bool hi = ro[j] != ro[0];
+                    float v = bv[j];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) v += (hi ? xb[u][k] : xa[u][k]) * w[j][k];
+                    o.h[j] = f2bf(apply_act(v, act));
+                    if (bnstat && j < nv) {
+                        const float dv = bf2f(o.h[j]) - ks[j];
+                        s1[j] += dv;
+                        s2[j] += dv * dv;
+                    }
+                }
+                if (nv == 8) {
+                    *reinterpret_cast<uint4*>(Y + e) = o.u4;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j < nv) Y[e + j] = o.h[j];
+                }
+            }
+        }
+    }
+    if (bnstat) {
+        __shared__ float red[2 * 2048];
+        if (active) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                red[q * 8 * N + 8 * i + j] = s1[j];
+                red[2048 + q * 8 * N + 8 * i + j] = s2[j];
+            }
+        }
+        __syncthreads();
+        float* ws = reinterpret_cast<float*>(d.aux);
+        for (int c = t; c < N; c += 256) {
+            float a = 0.f, b = 0.f;
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    a += red[g * 8 * N + c + m * N];
+                    b += red[2048 + g * 8 * N + c + m * N];
+                }
+            atomicAdd(ws + c, a);
+            atomicAdd(ws + N + c, b);
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc* __restrict__ descs,
+                                                                 const int4* __restrict__ tiles) {
+    // WGRAD dims: M = F (rows of dW), N = K (columns), K = reduction rows; dZ = dY * act'(Y)
+    __shared__ float red[(K + 1) * 2048];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const int F = (int)d.M, R = (int)d.K, act = (int)d.act;
+    const int ldx = (int)d.C;
+    const int t = threadIdx.x, G = 256 / F, q = t / F, i = t - q * F;
+    const bool active = q < G;
+    const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
+    const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
+    const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
+    float* dbias = reinterpret_cast<float*>(d.bias);
+    int ro[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ro[j] = (8 * i + j) / F;
+    float acc[8 * (K + 1)];
+#pragma unroll
+    for (int j = 0; j < 8 * (K + 1); ++j) acc[j] = 0.f;
+    const int64_t total = (int64_t)R * F;
+    const int r0 = td.y * NARROW_WROWS, r1 = min(R, r0 + NARROW_WROWS);
+    const int sr0 = r0 / 8, sr1 = (r1 + 7) / 8;
+    if (active) {
+        constexpr int U = NARROW_SR_U;
+        union V8 { uint4 u; bf16_t h[8]; };
+        for (int sb = sr0 + q; sb < sr1; sb += U * G) {
+            V8 g[U], y[U];
+            float xa[U][K], xb[U][K];
+            int nv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int sr = sb + u * G;
+                const int64_t e = (int64_t)sr * 8 * F + 8 * i;
+                nv[u] = sr < sr1 ? (int)max((int64_t)0, min((int64_t)8, total - e)) : 0;
+                g[u].u = make_uint4(0, 0, 0, 0);
+                y[u].u = make_uint4(0, 0, 0, 0);
+                if (nv[u] == 8) {
+                    g[u].u = *reinterpret_cast<const uint4*>(dY + e);
+                    if (act != ACT_LINEAR) y[u].u = *reinterpret_cast<const uint4*>(Yv + e);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j < nv[u]) {
+                            g[u].h[j] = dY[e + j];
+                            if (act != ACT_LINEAR) y[u].h[j] = Yv[e + j];
+                        }
+                }
+                const int ra = min(R - 1, min(sr, sr1 - 1) * 8 + ro[0]), rb = min(R - 1, ra + 1);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    xa[u][k] = bf2f(X[(int64_t)ra * ldx + k]);
+                    xb[u][k] = bf2f(X[(int64_t)rb * ldx + k]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float gz = bf2f(g[u].h[j]);          // 0 past the end
+                    if (act != ACT_LINEAR) gz = bf2f(f2bf(gz * act_grad_from_y(bf2f(y[u].h[j]), act)));
+                    const bool hi = ro[j] != ro[0];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) acc[j * K + k] += gz * (hi ? xb[u][k] : xa[u][k]);
+                    acc[8 * K + j] += gz;
+                }
+            }
+        }
+        // quantity p (k < K: weight column k, K: bias) of slot q * 8F + 8i + j
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) red[k * 2048 + q * 8 * F + 8 * i + j] = acc[j * K + k];
+            red[K * 2048 + q * 8 * F + 8 * i + j] = acc[8 * K + j];
+        }
+    }
+    __syncthreads();
+    for (int o = t; o < F * (K + 1); o += 256) {
+        const int c = o / (K + 1), p = o - c * (K + 1);
+        float v = 0.f;
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v += red[p * 2048 + g * 8 * F + c + m * F];
+        if (p < K) atomicAdd(reinterpret_cast<float*>(d.out) + (int64_t)c * K + p, v);
+        else if (dbias) atomicAdd(dbias + c, v);
+    }
+}
+
 // ==================================================================================================
 // LDS-tiled GEMM for 1x1 / Dense problems (row-major A[M][K] with row stride C, B[N][K]):
 //   FWD   : Y = act(A . B^T + bias)          A = layer input,  B = Wm
@@ -1615,14 +1820,15 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 }
 
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
-//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4),
+//                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4; + 100 staged, + 200 super-row),
 //                 7064 / 7128 for the LDS-tiled 1x1 kernel (BN = 64 / 128; tiles (prob, m tile, n tile, k range)),
 //                 8064 / 8128 the same for DGRAD with B = natural-layout weights [F][C] (BT)
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
 // variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
-//                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, F % 8 != 0); tiles (prob, row block, 0, 0)
+//                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, + 200: super-row form; F % 8 != 0);
+//                 tiles (prob, row block, 0, 0)
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
 //                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
@@ -1633,8 +1839,9 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     dim3 grid((unsigned)ntiles), block(256);
     if (mode == MODE_WGRAD && variant >= 4000000) {
         const int k = (variant - 4000000) % 100;
-        const bool st = (variant - 4000000) >= 100;
-#define NW(K_) if (k == K_) { if (st) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<K_, true>), grid, block, 0, s, dp, tp); \
+        const bool st = (variant - 4000000) >= 100, sr = (variant - 4000000) >= 200;
+#define NW(K_) if (k == K_) { if (sr) hipLaunchKernelGGL((g3_narrow_wgrad_sr_kernel<K_>), grid, block, 0, s, dp, tp); \
+                              else if (st) hipLaunchKernelGGL((g3_narrow_wgrad_kernel<K_, true>), grid, block, 0, s, dp, tp); \
                               else hipLaunchKernelGGL((g3_narrow_wgrad_kernel<K_, false>), grid, block, 0, s, dp, tp); }
         NW(1) else NW(2) else NW(3) else NW(4)
 #undef NW
@@ -1699,8 +1906,9 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     }
     if (mode == MODE_FWD && variant >= 6000 && variant < 7000) {
         const int k = (variant - 6000) % 100;
-        const bool st = (variant - 6000) >= 100;
-#define NF(K_) if (k == K_) { if (st) hipLaunchKernelGGL((g3_narrow_fwd_kernel<K_, true>), grid, block, 0, s, dp, tp); \
+        const bool st = (variant - 6000) >= 100, sr = (variant - 6000) >= 200;
+#define NF(K_) if (k == K_) { if (sr) hipLaunchKernelGGL((g3_narrow_fwd_sr_kernel<K_>), grid, block, 0, s, dp, tp); \
+                              else if (st) hipLaunchKernelGGL((g3_narrow_fwd_kernel<K_, true>), grid, block, 0, s, dp, tp); \
                               else hipLaunchKernelGGL((g3_narrow_fwd_kernel<K_, false>), grid, block, 0, s, dp, tp); }
         NF(1) else NF(2) else NF(3) else NF(4)
 #undef NF

@@ -288,9 +288,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             # + 100: LDS-staged rows when the narrow kernel's row width (N, or F for WGRAD) is not a
             # multiple of 8 (unaligned 16-B row chunks); measured faster for K <= 2 (Dense on the raw
             # genotype / image: FWD 3-4x), slower for K = 3, 4
+            # + 200: the super-row form (aligned 16-B accesses, no staging; row width > 8, any K)
             wide = N if mode == MODE_FWD else M
             st = wide % 8 != 0 and nk <= 2 and "nst" not in _OFF
-            v = (6000 if mode == MODE_FWD else 4000000) + nk + (100 if st else 0)
+            sr = wide % 8 != 0 and wide > 8 and "sr" not in _OFF
+            v = (6000 if mode == MODE_FWD else 4000000) + nk + (200 if sr else 100 if st else 0)
         elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
               and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
             v = 7128 if N > 64 else 7064          # LDS-tiled 1x1 / Dense GEMM
