@@ -10,7 +10,7 @@ from serann.ops import hip_ops as H
 def main():
     dev = "cuda"
     L, s = H.lib(), H.stream_handle()
-    for R, C in [(588000, 67), (363000, 64), (96000, 128), (750, 128), (363000, 16)]:
+    for R, C in [(588000, 67), (363000, 64), (96000, 128), (750, 128), (750, 256), (750, 37), (363000, 16)]:
         x = torch.randn(R, C, device=dev).bfloat16()
         y = torch.zeros_like(x); dy = torch.randn_like(x); dx = torch.zeros_like(x)
         f = lambda n: torch.zeros(n, device=dev)

@@ -155,7 +155,16 @@ __device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const 
 // partial sums, per-channel combination through LDS float atomics, one global atomic per channel
 // and block.  Works for any C (odd channel counts included).
 constexpr int BN_VEC_ELEMS = 16384;     // elements per block (super-rows per block = 2048 / C)
-constexpr int BN_RED_MULT = 4;          // statistics phases: BN_RED_MULT x BN_VEC_ELEMS per block
+constexpr int BN_RED_MULT = 4;          // statistics phases: BN_RED_MULT x BN_VEC_ELEMS per block ...
+constexpr int BN_STAT_SMALL = 64;       // ... unless the problem spans fewer blocks than this at 1x
+
+// rows-per-block multiplier of the statistics phases.  Large problems take BN_RED_MULT (1x: more
+// device-scope atomics per channel, measured slower; 8x: too few blocks, also slower).  Small ones
+// (the merged-branch BN on [B][D], a few blocks) are bound by the serial chain of loads in each
+// block and keep 1x: R = 750, C = 128 phase 4 drops from 16 to 7 us.
+__host__ __device__ __forceinline__ int bn_stat_mult(int nsr, int srb1) {
+    return (nsr + srb1 - 1) / srb1 < BN_STAT_SMALL ? 1 : BN_RED_MULT;
+}
 
 __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, float* sA, float* sB) {
     const int R = (int)d.R, C = (int)d.C;
@@ -168,8 +177,9 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     const int q = t / C, i = t - q * C;
     // the statistics phases (0, 4) walk BN_RED_MULT times more rows per block: every block ends with
     // 2C device-scope float atomics, which dominated those phases at 16K elements per block
-    const int srb = max(1, (BN_VEC_ELEMS / 8) / C) * ((phase == 0 || phase == 4) ? BN_RED_MULT : 1);
     const int nsr = (R + 7) / 8;
+    const int srb1 = max(1, (BN_VEC_ELEMS / 8) / C);
+    const int srb = srb1 * ((phase == 0 || phase == 4) ? bn_stat_mult(nsr, srb1) : 1);
     const int sr0 = tile * srb, sr1 = min(nsr, sr0 + srb);
     const int64_t total = (int64_t)R * C;
     const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);

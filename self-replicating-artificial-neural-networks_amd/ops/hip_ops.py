@@ -81,6 +81,7 @@ BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256
 
 
 BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block
+BN_STAT_SMALL = 64     # aux.hip: ... unless the problem spans fewer blocks than this at 1x
 
 
 def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
@@ -89,8 +90,10 @@ def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
     c = max(int(channels), 1)
     if c > 256:
         return red_chunks(rows, c)
-    srb = max(1, (BN_VEC_ELEMS // 8) // c) * (BN_RED_MULT if stats else 1)
-    return -(-(-(-int(rows) // 8)) // srb)
+    nsr = -(-int(rows) // 8)
+    srb1 = max(1, (BN_VEC_ELEMS // 8) // c)
+    srb = srb1 * (1 if not stats or -(-nsr // srb1) < BN_STAT_SMALL else BN_RED_MULT)
+    return -(-nsr // srb)
 
 
 def pool_units(elements: int, channels: int) -> int:
