@@ -14,7 +14,7 @@ def main():
         x = torch.randn(R, C, device=dev).bfloat16()
         y = torch.zeros_like(x); dy = torch.randn_like(x); dx = torch.zeros_like(x)
         f = lambda n: torch.zeros(n, device=dev)
-        gamma, beta, mm, mv, mean, invstd, ws, dg, db = f(C) + 1, f(C), f(C), f(C) + 1, f(C), f(C), f(4 * C), f(C), f(C)
+        gamma, beta, mm, mv, mean, invstd, ws, dg, db = f(C) + 1, f(C), f(C), f(C) + 1, f(C), f(C), f(2 * H.BN_WS_STRIPES * C), f(C), f(C)
         row = dict(x=x.data_ptr(), y=y.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), gamma=gamma.data_ptr(),
                    beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(),
                    invstd=invstd.data_ptr(), ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C,

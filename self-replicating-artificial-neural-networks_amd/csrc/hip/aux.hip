@@ -166,6 +166,17 @@ __host__ __device__ __forceinline__ int bn_stat_mult(int nsr, int srb1) {
     return (nsr + srb1 - 1) / srb1 < BN_STAT_SMALL ? 1 : BN_RED_MULT;
 }
 
+// Statistics workspace of the vectorised path: BN_WS_STRIPES copies of the 2C sums; block `tile` adds
+// into copy tile % BN_WS_STRIPES (a quarter of the same-address atomics: they serialise in L2 and
+// bounded the statistics phases), readers sum the copies.  Producers fused into other kernels
+// (GF_BNSTAT) add into copy 0.
+__device__ __forceinline__ float wsum(const float* ws, int C, int idx) {
+    float v = 0.f;
+#pragma unroll
+    for (int s = 0; s < BN_WS_STRIPES; ++s) v += ws[s * 2 * C + idx];
+    return v;
+}
+
 __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, float* sA, float* sB) {
     const int R = (int)d.R, C = (int)d.C;
     const int flags = (int)d.flags;
@@ -184,6 +195,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     const int64_t total = (int64_t)R * C;
     const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
     float* ws = reinterpret_cast<float*>(d.ws);
+    float* wsw = ws + (tile % BN_WS_STRIPES) * 2 * C;     // this block's statistics copy
     int ch[8];
     {
         int c = (8 * i) % C;
@@ -199,9 +211,9 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
             float mu, var;
             if (phase == 2) {
                 const float K = bf2f(x[c]);
-                const float m1 = ws[c] / Rf;
+                const float m1 = wsum(ws, C, c) / Rf;
                 mu = K + m1;
-                var = fmaxf(ws[C + c] / Rf - m1 * m1, 0.f);
+                var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
             } else {
                 mu = reinterpret_cast<const float*>(d.mm)[c];
                 var = reinterpret_cast<const float*>(d.mv)[c];
@@ -217,7 +229,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
             const float mu = reinterpret_cast<const float*>(d.mean)[c];
             const float is = reinterpret_cast<const float*>(d.invstd)[c];
             const float gg = ((flags & 1) ? reinterpret_cast<const float*>(d.gamma)[c] : 1.f) * is;
-            const float ma = ws[c] / Rf, mb = ws[C + c] / Rf;
+            const float ma = wsum(ws, C, c) / Rf, mb = wsum(ws, C, C + c) / Rf;
             a = gg;                                            // k1
             b = -gg * is * mb;                                 // k2
             sA[256 + c] = -gg * (ma - mu * is * mb);           // k3
@@ -233,9 +245,9 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
         float* invstd = reinterpret_cast<float*>(d.invstd);
         for (int c = t; c < C; c += 256) {
             const float K = bf2f(x[c]);
-            const float m1 = ws[c] / Rf;
+            const float m1 = wsum(ws, C, c) / Rf;
             const float mu = K + m1;
-            const float var = fmaxf(ws[C + c] / Rf - m1 * m1, 0.f);
+            const float var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
             mm[c] = mm[c] * mom + mu * (1.f - mom);
             mv[c] = mv[c] * mom + var * (Rf / (Rf - (1.f + eps))) * (1.f - mom);
             mean[c] = mu;
@@ -244,8 +256,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     }
     if (phase == 5 && tile == 0) {
         for (int c = t; c < C; c += 256) {
-            if (flags & 1) reinterpret_cast<float*>(d.dgamma)[c] += ws[C + c];
-            if (flags & 2) reinterpret_cast<float*>(d.dbeta)[c] += ws[c];
+            if (flags & 1) reinterpret_cast<float*>(d.dgamma)[c] += wsum(ws, C, C + c);
+            if (flags & 2) reinterpret_cast<float*>(d.dbeta)[c] += wsum(ws, C, c);
         }
     }
     __syncthreads();
@@ -359,8 +371,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
             for (int s = t; s < 2048; s += 256) { a += r0[s]; b += r1[s]; }
             for (int o = C; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
             if (lane < C) {
-                atomicAdd(&ws[lane], a);
-                atomicAdd(&ws[C + lane], b);
+                atomicAdd(&wsw[lane], a);
+                atomicAdd(&wsw[C + lane], b);
             }
             return;
         }
@@ -372,8 +384,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
                     a += r0[g * 8 * C + c + k * C];
                     b += r1[g * 8 * C + c + k * C];
                 }
-            atomicAdd(&ws[c], a);
-            atomicAdd(&ws[C + c], b);
+            atomicAdd(&wsw[c], a);
+            atomicAdd(&wsw[C + c], b);
         }
     }
 }

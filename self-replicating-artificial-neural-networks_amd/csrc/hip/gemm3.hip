@@ -1196,7 +1196,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
             red[(8 + j) * 256 + t] = active ? s2[j] : 0.f;
         }
         __syncthreads();
-        float* ws = reinterpret_cast<float*>(d.aux);
+        float* ws = reinterpret_cast<float*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 2 * N;   // stripe
         for (int o = t; o < FC * 8; o += 256) {
             const int ch = o >> 3, j = o & 7, c = ch * 8 + j;
             if (c >= N) continue;
@@ -1441,7 +1441,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
             }
         }
         __syncthreads();
-        float* ws = reinterpret_cast<float*>(d.aux);
+        float* ws = reinterpret_cast<float*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 2 * N;   // stripe
         for (int c = t; c < N; c += 256) {
             float a = 0.f, b = 0.f;
             for (int g = 0; g < G; ++g)

@@ -376,8 +376,8 @@ class HipPopulationEngine(PopulationEngine):
         for lay, rec in zip(self.layouts, bufs):
             for nid, d in rec["bn"].items():
                 c = lay.ir.node(nid).attrs["channels"]
-                d["ws"] = ws.alloc(2 * c)
-                d["wsb"] = ws.alloc(2 * c)
+                d["ws"] = ws.alloc(2 * c * H.BN_WS_STRIPES)
+                d["wsb"] = ws.alloc(2 * c * H.BN_WS_STRIPES)
         act.materialize(zero=True)
         grad.materialize(zero=True)
         f32.materialize(zero=True)
@@ -715,7 +715,7 @@ class HipPopulationEngine(PopulationEngine):
                             # a narrow-kernel output that feeds a BatchNormalization: the BN statistics
                             # (phase 0) are accumulated by the producing kernel itself
                             bnc = bn_consumer[o].get(n.id)
-                            if (train and bnc is not None and FUSE_BN_STATS
+                            if (train and bnc is not None and FUSE_BN_STATS and F <= 256
                                     and H.narrow_k(g_rows[-1], H.MODE_FWD, M, F, K) is not None):
                                 g_rows[-1]["aux"] = mem["ws"].ptr(rec["bn"][bnc]["ws"])
                                 g_rows[-1]["flags"] |= H.GF_BNSTAT

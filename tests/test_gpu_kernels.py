@@ -241,7 +241,7 @@ def test_bn_train_infer_backward(RC):
     beta = torch.randn(C, device=DEV)
     mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, invstd = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-    ws = torch.zeros(4 * C, device=DEV)
+    ws = torch.zeros(2 * H.BN_WS_STRIPES * C, device=DEV)
     y = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
     dy = torch.randn(R, C, device=DEV).bfloat16()
     dx = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
