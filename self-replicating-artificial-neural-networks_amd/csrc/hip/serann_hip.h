@@ -74,7 +74,7 @@ void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t
 struct ActBwdDesc { int64_t dy, y, dz, dbias, M, N, act, flags; };          // flags: 1 = write dz
 // BatchNorm statistics workspace: BN_WS_STRIPES copies of [2][C] fp32 sums (C <= 256 problems), one
 // per block-index residue, summed by the readers (aux.hip wsum)
-constexpr int BN_WS_STRIPES = 4;
+constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
     int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx
