@@ -156,12 +156,12 @@ __device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const 
 // and block.  Works for any C (odd channel counts included).
 constexpr int BN_VEC_ELEMS = 16384;     // elements per block (super-rows per block = 2048 / C)
 constexpr int BN_RED_MULT = 4;          // statistics phases: BN_RED_MULT x BN_VEC_ELEMS per block ...
-constexpr int BN_STAT_SMALL = 512;      // ... unless the problem spans fewer blocks than this at 1x
+constexpr int BN_STAT_SMALL = 2048;     // ... unless the problem spans fewer blocks than this at 1x
 
 // rows-per-block multiplier of the statistics phases.  Large problems take BN_RED_MULT (1x: more
 // device-scope atomics per channel, measured slower; 8x: too few blocks, also slower).  Small ones
-// (< 512 blocks at 1x, e.g. the merged-branch BN on [B][D]) are bound by the serial chain of loads in each
-// block / too few CUs and keep 1x: [750][128] phase 4 16 -> 7 us, [363000][16] 23 -> 16 us (with the
+// (< 2048 blocks at 1x, e.g. the merged-branch BN on [B][D]) are bound by the serial chain of loads in each
+// block / too few CUs and keep 1x: [750][128] phase 4 16 -> 7 us, [96000][128] phase 0 21 -> 9 us (with the
 // striped workspace below; before striping, 1x lost on mid-size problems).
 __host__ __device__ __forceinline__ int bn_stat_mult(int nsr, int srb1) {
     return (nsr + srb1 - 1) / srb1 < BN_STAT_SMALL ? 1 : BN_RED_MULT;

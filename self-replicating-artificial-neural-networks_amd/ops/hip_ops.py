@@ -82,7 +82,7 @@ BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256
 
 BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block
 BN_WS_STRIPES = 8      # serann_hip.h: copies of the [2][C] BN statistics workspace (C <= 256)
-BN_STAT_SMALL = 512    # aux.hip: ... unless the problem spans fewer blocks than this at 1x
+BN_STAT_SMALL = 2048    # aux.hip: ... unless the problem spans fewer blocks than this at 1x
 
 
 def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
