@@ -46,13 +46,12 @@ def main(argv=None, script=None):
     from ..utils.db import ExperimentDB
 
     comm = make_comm()
-    seed = int(args.random_seed or config["random_seed"])
-    np.random.seed(seed)
     results_dir = Path(config["experiment_results_dir"])
     if comm.is_root:
         results_dir.mkdir(exist_ok=True, parents=True)
 
     start_generation = 0
+    stored_seed = None
     if args.resume_experiment_id is None:
         if not args.parameters:
             raise SystemExit("--parameters is required for a new experiment")
@@ -66,18 +65,30 @@ def main(argv=None, script=None):
         state = None
         if comm.is_root:
             start_generation = db.get_generations_count()
+            info = db.get_last_execution_info()
+            # the per-organism weight-init and epoch-permutation seeds derive from random_seed: a resume
+            # without -s continues with the seed the run was started with
+            if "random_seed" in info and info["random_seed"] is not None and str(info["random_seed"]) != "nan":
+                stored_seed = int(info["random_seed"])
             if args.parameters is not None:
                 with open(args.parameters) as f:
                     parameters = json.load(f)
             else:
-                info = db.get_last_execution_info()
                 parameters = {k: v for k, v in info.drop("start_time").items()}
                 for k in ("host_name", "encodings_dataset", "tokens_vocabulary", "ribosomal_autoencoder", "random_seed"):
                     parameters.pop(k, None)
                 if start_generation == parameters["num_generations"]:
                     parameters["num_generations"] *= 2
-            state = (start_generation, parameters)
-        start_generation, parameters = comm.broadcast_object(state)
+            state = (start_generation, parameters, stored_seed)
+        start_generation, parameters, stored_seed = comm.broadcast_object(state)
+
+    if args.random_seed is not None:
+        seed = int(args.random_seed)
+    elif stored_seed is not None:
+        seed = stored_seed
+    else:
+        seed = int(config["random_seed"])
+    np.random.seed(seed)
 
     s = setup(parameters, engine=args.engine, codec=args.codec, comm=comm, n_train=args.data_subset)
     parameters["host_name"] = socket.gethostname()

@@ -170,7 +170,7 @@ __host__ __device__ __forceinline__ int bn_stat_mult(int nsr, int srb1) {
 // Statistics workspace of the vectorised path: BN_WS_STRIPES copies of the 2C sums; block `tile` adds
 // into copy tile % BN_WS_STRIPES (an eighth of the same-address atomics: they serialise in L2 and
 // bounded the statistics phases), readers sum the copies.  Producers fused into other kernels
-// (GF_BNSTAT) add into copy 0.
+// (GF_BNSTAT, gemm3.hip) stripe the same way, by their own blockIdx.x % BN_WS_STRIPES.
 __device__ __forceinline__ float wsum(const float* ws, int C, int idx) {
     float v = 0.f;
 #pragma unroll

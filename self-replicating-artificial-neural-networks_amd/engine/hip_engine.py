@@ -1204,23 +1204,37 @@ class HipPopulationEngine(PopulationEngine):
             tmp = Plan()
             tmp.launches = pl.launches[:pl.fwd_count]
             tmp.run()
-            self._run_loss(pl, True, B)
+            if pl.loss is not None:
+                self._run_loss(pl, True, pl.loss[2])
             tmp.launches = pl.launches[pl.fwd_count:]
             tmp.run()
 
-        def step():
+        # Keras trains the last step of an epoch on the true remainder (split % B rows), so that step has
+        # its own plan (BatchNorm batch statistics, loss mean, gradients and accuracy over Br rows) and
+        # its own activation buffers; it reads the first Br rows of the shared batch buffers.
+        full_steps = split // B
+        Br = split - full_steps * B
+        rem_plans, rem_ws = None, None
+        if Br > 0 and steps > full_steps:
+            mem_r = self._alloc_buffers(Br, with_grads=True)
+            self._train_mem_rem = mem_r
+            rem_plans = [self._build_plan("train", Br, mem_r, inputs, yb.data_ptr(), targets, metrics, orgs=g_)
+                         for g_ in groups]
+            rem_ws = mem_r["ws"].t
+
+        def step(pls=plans, nb=B, wsb=ws, base=0, ctr=True):
             s = H.stream_handle()
             L.gather_batch(dd["train_x"].data_ptr(), dd["train_g"].data_ptr(), dd["train_y"].data_ptr(),
-                           perm_t.data_ptr(), counter.data_ptr(), 0, B, split, xcols, gcols, xb.data_ptr(),
-                           gb.data_ptr(), yb.data_ptr(), s)
-            L.memset32(ws.data_ptr(), ws.numel(), s)
-            if len(plans) == 1:
-                run_plan(plans[0])
+                           perm_t.data_ptr(), counter.data_ptr() if ctr else 0, base, nb, split, xcols, gcols,
+                           xb.data_ptr(), gb.data_ptr(), yb.data_ptr(), s)
+            L.memset32(wsb.data_ptr(), wsb.numel(), s)
+            if len(pls) == 1:
+                run_plan(pls[0])
             else:
                 main = torch.cuda.current_stream()
                 for st in streams:
                     st.wait_stream(main)
-                for pl, st in zip(plans, streams):
+                for pl, st in zip(pls, streams):
                     with torch.cuda.stream(st):
                         run_plan(pl)
                 for st in streams:
@@ -1231,7 +1245,10 @@ class HipPopulationEngine(PopulationEngine):
                    cfg.eps, s)
             L.counter_add(counter.data_ptr(), 1, s)
 
-        use_graph = split % B == 0 and steps == split // B
+        def remainder_step():
+            step(rem_plans, Br, rem_ws, full_steps * B, False)
+
+        use_graph = full_steps > 1
         graph = None
         self.timings["plan_s"] = time.perf_counter() - t_plan
         self.timings["launches_per_step"] = sum(len(pl.launches) for pl in plans) + 5
@@ -1247,7 +1264,8 @@ class HipPopulationEngine(PopulationEngine):
             perm_t.copy_(torch.from_numpy(perm))
             counter.zero_()
             metrics.zero_()
-            if use_graph and graph is None and steps > 1:
+            nfull = min(steps, full_steps)
+            if use_graph and graph is None and nfull > 1:
                 # warm one step eagerly (first-touch), then capture
                 step()
                 total += 1
@@ -1258,14 +1276,17 @@ class HipPopulationEngine(PopulationEngine):
                     with torch.cuda.graph(graph, stream=s_):
                         step()
                 torch.cuda.current_stream().wait_stream(s_)
-                remaining = steps - 1
+                remaining = nfull - 1
             else:
-                remaining = steps
+                remaining = nfull
             for _ in range(remaining):
                 if graph is not None:
                     graph.replay()
                 else:
                     step()
+                total += 1
+            if rem_plans is not None and steps > nfull:
+                remainder_step()
                 total += 1
             m = metrics.cpu().numpy()
             train_acc = m[:, 1] / np.maximum(m[:, 3], 1)

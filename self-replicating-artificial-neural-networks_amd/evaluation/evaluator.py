@@ -33,6 +33,14 @@ LB_REGEX = re.compile(r"loss_balance *= *([0-9]+\.[0-9]+?)(\s|$)")
 EMPTY = {"classification_accuracy": np.nan, "offspring_survival": {}, "mutation_rate": {}}
 
 
+def genotype_key(genotype) -> str:
+    """Stable identity of a genotype: its bits as a hex string (NaN / non-binary loci kept distinct)."""
+    g = np.asarray(genotype, np.float64)
+    if np.all((g == 0) | (g == 1)):
+        return np.packbits(g.astype(np.uint8)).tobytes().hex()
+    return g.tobytes().hex()
+
+
 def probabilistic_proofreading(parent, offspring, ec_factor: float, rng: np.random.RandomState):
     """Revert a random fraction ``ec_factor`` of the loci that differ from the parent (common/logic.py:6-14)."""
     offspring = np.array(offspring, copy=True)
@@ -103,7 +111,10 @@ class SerannEvaluator:
                 irs.append(r.ir)
                 owners.append((i, e))
         if irs:
-            seeds = [organism_seed(self.seed, i, f"eval{e}") for i, e in owners]
+            # keyed on the genotype itself (not its position in this batch), so a genotype gets the same
+            # replica initialisations however run_many batches / de-duplicates / shards the sample
+            keys = {i: genotype_key(genotypes[i]) for i, _ in owners}
+            seeds = [organism_seed(self.seed, keys[i], f"eval{e}") for i, e in owners]
             eng = make_engine(self.engine, irs, seeds, self.device, self.cfg)
             try:
                 fit = eng.fit(self.data, self.cfg)

@@ -158,7 +158,7 @@ class Experiment:
             if self._comm.is_root and self._db is not None:
                 self._db.save_resume_state(generation_number, {
                     "next_generation": next_generation, "pool_size": offspring_pool_size,
-                    "rng": self._rng.get_state()})
+                    "rng": self._rng.get_state(), "random_seed": self._random_seed})
             current = next_generation
             record["seconds"] = time.perf_counter() - t0
             record["phases"] = timer.reset()

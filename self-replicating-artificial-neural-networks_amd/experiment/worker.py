@@ -19,6 +19,16 @@ from ..engine.base import TrainConfig, replication_image_rows
 from ..genome.ir import OrganismIR
 
 
+def replication_bits(outputs: np.ndarray) -> np.ndarray:
+    """Sigmoid replication outputs -> offspring bits, ``round(clip(o, 0, 1))`` (experiment.py:206-209).
+
+    A diverged organism (NaN / inf logits) has non-finite outputs.  The reference keeps NaN loci in the
+    float genotype it stores (its DB reader parses 'nan'); offspring genotypes here travel bit-packed,
+    so a non-finite locus is mapped explicitly: NaN -> 0, +inf -> 1, -inf -> 0 (docs/deviations.md)."""
+    o = np.nan_to_num(np.asarray(outputs, np.float64), nan=0.0, posinf=1.0, neginf=0.0)
+    return np.round(np.clip(o, 0, 1)).astype(np.uint8)
+
+
 def organism_seed(random_seed: int, generation: int, organism_id: str) -> int:
     h = hashlib.blake2b(f"{random_seed}:{generation}:{organism_id}".encode(), digest_size=8).digest()
     return int.from_bytes(h, "little") & 0x7FFFFFFF
@@ -86,7 +96,7 @@ class ShardWorker:
                           for q in pos]
                 outs = engine.replicate(np.asarray(genotypes, np.float32), images, cfg)
                 for p, o in enumerate(outs):
-                    offspring[p] = np.round(np.clip(o, 0, 1)).astype(np.uint8)
+                    offspring[p] = replication_bits(o)
                 replication_time = time.perf_counter() - t0
         finally:
             engine.close()

@@ -7,13 +7,15 @@ generation, index ``id``), ``generations`` (one row per generation), ``model_met
 Differences (documented): uses the stdlib ``sqlite3`` driver (pandas' sqlite fallback) instead of
 SQLAlchemy; DB errors are *raised* unless ``swallow_errors=True`` (the reference prints and
 continues); an additive ``resume_state`` table stores the packed offspring
-genotypes and RNG state so that resume is exact without retraining.
+genotypes and RNG state so that resume is exact without retraining.  The resume state is
+plain data -- a JSON text column and an ``.npz`` blob read with ``allow_pickle=False`` -- so opening a
+shared results DB never unpickles anything.
 """
 from __future__ import annotations
 
 import ast
+import io
 import json
-import pickle
 import sqlite3
 from contextlib import contextmanager
 
@@ -95,11 +97,24 @@ class ExperimentDB:
             metrics.assign(model=model_name).to_sql("model_metrics", conn, index=False, if_exists="append")
 
     def save_resume_state(self, generation: int, state: dict):
-        """Additive table: exact resume point after ``generation`` (next generation + RNG)."""
-        blob = pickle.dumps(state)
+        """Additive table: exact resume point after ``generation``.
+
+        ``state``: ``next_generation`` (DataFrame indexed by id with a ``genotype`` column of arrays),
+        ``pool_size``, ``rng`` (``RandomState.get_state()`` tuple), ``random_seed``."""
+        meta, arrays = _pack_resume_state(state)
+        buf = io.BytesIO()
+        np.savez(buf, **arrays)
         with self.db_connection() as conn:
-            conn.execute("create table if not exists resume_state (generation integer primary key, state blob)")
-            conn.execute("insert or replace into resume_state values (?, ?)", (int(generation), blob))
+            if self._table_exists(conn, "resume_state") and "meta" not in self._columns(conn, "resume_state"):
+                conn.execute("drop table resume_state")      # pre-plain-data format: never read
+            conn.execute("create table if not exists resume_state "
+                         "(generation integer primary key, meta text, arrays blob)")
+            conn.execute("insert or replace into resume_state values (?, ?, ?)",
+                         (int(generation), json.dumps(meta), buf.getvalue()))
+
+    @staticmethod
+    def _columns(conn, table):
+        return [r[1] for r in conn.execute(f"pragma table_info({table})").fetchall()]
 
     # ---- readers -------------------------------------------------------------------------------
     def get_last_execution_info(self) -> pd.Series:
@@ -149,7 +164,58 @@ class ExperimentDB:
 
     def get_resume_state(self, generation: int):
         with self.db_connection() as conn:
-            if not self._table_exists(conn, "resume_state"):
+            if not self._table_exists(conn, "resume_state") or "meta" not in self._columns(conn, "resume_state"):
                 return None
-            row = conn.execute("select state from resume_state where generation = ?", (int(generation),)).fetchone()
-        return pickle.loads(row[0]) if row else None
+            row = conn.execute("select meta, arrays from resume_state where generation = ?",
+                               (int(generation),)).fetchone()
+        if not row:
+            return None
+        with np.load(io.BytesIO(row[1]), allow_pickle=False) as z:
+            arrays = {k: z[k] for k in z.files}
+        return _unpack_resume_state(json.loads(row[0]), arrays)
+
+
+def _json_value(v):
+    if v is None or (isinstance(v, float) and np.isnan(v)):
+        return None
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return None if np.isnan(v) else float(v)
+    if isinstance(v, (np.bool_,)):
+        return bool(v)
+    return v
+
+
+def _pack_resume_state(state: dict):
+    df = state["next_generation"]
+    other = [c for c in df.columns if c != "genotype"]
+    meta = {"ids": [str(i) for i in df.index], "index_name": df.index.name,
+            "columns": {c: [_json_value(v) for v in df[c].tolist()] for c in other},
+            "column_order": list(df.columns), "pool_size": int(state["pool_size"]),
+            "random_seed": None if state.get("random_seed") is None else int(state["random_seed"])}
+    arrays = {"genotype": np.stack([np.asarray(g, np.float64) for g in df["genotype"]])
+              if len(df) else np.zeros((0, 0))}
+    rng = state.get("rng")
+    if rng is not None:
+        name, keys, pos, has_gauss, cached = rng
+        meta["rng"] = {"name": str(name), "pos": int(pos), "has_gauss": int(has_gauss), "cached": float(cached)}
+        arrays["rng_keys"] = np.asarray(keys, np.uint32)
+    return meta, arrays
+
+
+def _unpack_resume_state(meta: dict, arrays: dict) -> dict:
+    import pandas as pd_
+    ids = meta["ids"]
+    df = pd_.DataFrame(index=pd_.Index(ids, name=meta.get("index_name")))
+    for c in meta["column_order"]:
+        if c == "genotype":
+            df["genotype"] = [arrays["genotype"][i] for i in range(len(ids))]
+        else:
+            vals = meta["columns"][c]
+            df[c] = [np.nan if v is None and c != "parent_id" else v for v in vals]
+    out = {"next_generation": df, "pool_size": meta["pool_size"], "random_seed": meta.get("random_seed")}
+    if "rng" in meta:
+        r = meta["rng"]
+        out["rng"] = (r["name"], arrays["rng_keys"], r["pos"], r["has_gauss"], r["cached"])
+    return out

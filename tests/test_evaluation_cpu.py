@@ -111,3 +111,24 @@ def test_load_experiment_data_by_path(experiment):
     j = load_experiment_data(path, deep_evaluations=ev)          # cached frame + evaluation join
     assert j.loc[j["genotype_hex"] == ev["genotype_hex"][0], "fitness"].eq(0.5).all()
     assert j["fitness"].isna().sum() == (j["genotype_hex"] != ev["genotype_hex"][0]).sum()
+
+
+def test_replica_seeds_follow_the_genotype(experiment):
+    """A genotype's replica initialisations (and so its accuracies) do not depend on its position in the
+    evaluated batch: evaluating X alone or after another genotype gives the same accuracies."""
+    from serann.evaluation.evaluator import SerannEvaluator
+    df, data, codec, p, _ = experiment
+    ep = {k: p[k] for k in ("genotype_size", "error_correction_probability", "classification_image_dimensions",
+                            "num_classification_classes", "training_epochs", "training_batch_size")}
+    ok = df[(df["is_valid"] == True) & (df["is_overweight"] == False)]  # noqa: E712
+    hexes = ok["genotype_hex"].drop_duplicates()
+    assert len(hexes) >= 1
+    x = np.asarray(ok.loc[hexes.index[0], "genotype"], np.float64)
+    y = 1.0 - x
+
+    def ev():
+        return SerannEvaluator(ep, data, codec, num_evaluations=2, replications_per_evaluation=2, engine="torch",
+                               device="cpu", train_cfg=TrainConfig(epochs=1, batch_size=200))
+    alone = ev().evaluate_many([x])[0]
+    second = ev().evaluate_many([y, x])[1]
+    assert alone["classification_accuracy"] == second["classification_accuracy"]

@@ -123,3 +123,62 @@ def test_fault_spec_parsing():
     maybe_inject(2, rank=1, spec="generation=3,rank=1")     # other generation: no fault
     with pytest.raises(InjectedFault):
         maybe_inject(3, rank=1, spec="generation=3,rank=1")
+
+
+def test_cli_resume_keeps_started_seed(tmp_path, monkeypatch):
+    """A run started with ``-s N``, killed, and resumed with ``-r <id>`` alone must continue with seed N
+    (organism weight-init and epoch-permutation seeds derive from it): same rows as an uninterrupted run."""
+    import json
+
+    from serann.cli import run_experiment as cli
+    from serann.config import experiment_config
+    from serann.utils.faults import InjectedFault
+    monkeypatch.setitem(experiment_config, "experiment_results_dir", str(tmp_path))
+    p = default_parameters("example")
+    p.update(num_seranns=3, num_generations=3, training_epochs=1)
+    pf = tmp_path / "p.json"
+    pf.write_text(json.dumps(p))
+    common = ["--engine", "torch", "--codec", "table", "--data-subset", "1200"]
+    ref_id = cli.main(["-p", str(pf), "-s", "4242", *common])
+    monkeypatch.setenv("SERANN_FAULT_INJECT", "generation=2")
+    with pytest.raises(InjectedFault):
+        cli.main(["-p", str(pf), "-s", "4242", *common])
+    monkeypatch.delenv("SERANN_FAULT_INJECT")
+    crashed = [f.stem for f in tmp_path.glob("*.sqlite") if f.stem != ref_id]
+    assert len(crashed) == 1
+    cli.main(["-r", crashed[0], *common])
+    cols = "id, genotype, source_code, parent_id, generation, num_offspring, classification_validation_accuracy"
+    a = pd.read_sql(f"select {cols} from serann", sqlite3.connect(tmp_path / f"{ref_id}.sqlite"))
+    b = pd.read_sql(f"select {cols} from serann", sqlite3.connect(tmp_path / f"{crashed[0]}.sqlite"))
+    pd.testing.assert_frame_equal(a, b)
+    info = pd.read_sql("select random_seed from execution_info", sqlite3.connect(tmp_path / f"{crashed[0]}.sqlite"))
+    assert [int(s) for s in info["random_seed"]] == [4242, 4242]
+
+
+def test_resume_state_is_plain_data(tmp_path):
+    """The resume state round-trips through JSON + npz (no pickle), NaN genotypes included."""
+    db = ExperimentDB(tmp_path / "r.sqlite")
+    df = pd.DataFrame({"genotype": [np.array([0.0, 1.0, np.nan]), np.array([1.0, 1.0, 0.0])],
+                       "source_code": ["a=1", "b=2"], "parent_id": [None, "p1"],
+                       "genotype_hamming_distance_from_parent": [np.nan, 2.0]},
+                      index=pd.Index(["i0", "i1"], name="id"))
+    rng = np.random.RandomState(3)
+    rng.normal()
+    db.save_resume_state(4, {"next_generation": df, "pool_size": 7, "rng": rng.get_state(), "random_seed": 99})
+    st = db.get_resume_state(4)
+    assert st["pool_size"] == 7 and st["random_seed"] == 99
+    got = st["next_generation"]
+    assert list(got.index) == ["i0", "i1"] and list(got.columns) == list(df.columns)
+    assert np.array_equal(got["genotype"].iloc[0], df["genotype"].iloc[0], equal_nan=True)
+    assert got["parent_id"].iloc[0] is None and got["parent_id"].iloc[1] == "p1"
+    r2 = np.random.RandomState()
+    r2.set_state(st["rng"])
+    assert r2.normal() == rng.normal()
+    blob = sqlite3.connect(db.db_path).execute("select arrays from resume_state").fetchone()[0]
+    assert blob[:2] == b"PK"                                  # an npz archive
+
+
+def test_replication_bits_non_finite():
+    from serann.experiment.worker import replication_bits
+    o = np.array([[0.2, 0.7, np.nan, np.inf, -np.inf, 1.5, -0.3]])
+    assert replication_bits(o).tolist() == [[0, 1, 0, 1, 0, 1, 0]]

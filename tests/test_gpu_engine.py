@@ -120,6 +120,43 @@ def test_fit_graph_replay_learns():
     assert outs[0].shape == (20, 100) and np.all((outs[0] >= 0) & (outs[0] <= 1))
 
 
+def test_fit_remainder_batch_matches_torch():
+    """A batch size that does not divide the training split: the last step of each epoch trains on
+    the true remainder (Keras semantics), in the HIP engine as in the torch oracle.  BatchNorm moving
+    statistics carry ~25 % of their value from the last of 4 steps, so a remainder step padded with
+    duplicated rows would show up here."""
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    from serann.engine.torch_engine import TorchPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=1000, n_test=200, seed=9),
+                           n_train=1000, n_test=200)
+    names = ("odd_channels_bn", "narrow_bn_x")
+    irs = [interpret(ARCHS[n]) for n in names]
+    seeds = [21, 22]
+    cfg = TrainConfig(epochs=1, batch_size=300)      # split 950 = 3 x 300 + 50
+    assert cfg.split(1000) % cfg.batch_size == 50
+    hip = HipPopulationEngine(irs, seeds, device="cuda", cfg=cfg,
+                              params=[init_params(ir, s) for ir, s in zip(irs, seeds)])
+    rh = hip.fit(data, cfg)
+    ref = TorchPopulationEngine(irs, seeds, device="cuda", cfg=cfg)
+    rr = ref.fit(data, cfg)
+    assert rh.steps == rr.steps == 4
+    for i, ir in enumerate(irs):
+        got = hip.export_params(i)
+        org = ref.orgs[i]
+        for n in ir.nodes:
+            if n.op != "bn":
+                continue
+            for k in ("moving_mean", "moving_variance"):
+                want = org.params[f"n{n.id}_{k}"].detach().cpu().numpy()
+                base = np.zeros_like(want) if k == "moving_mean" else np.ones_like(want)
+                # compare the accumulated update (the statistics start at 0 / 1)
+                err = _rel(got[n.id][k] - base, want - base)
+                assert err < 0.1, (names[i], n.id, k, err)
+    assert np.allclose(rh.train_acc, rr.train_acc, atol=0.05), (rh.train_acc, rr.train_acc)
+
+
 def test_adam_kernel_matches_keras_formula():
     from serann.ops import hip_ops as H
     lib = H.lib()

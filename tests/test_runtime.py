@@ -87,5 +87,8 @@ def test_db_roundtrip(tmp_path):
     assert list(back.index) == ["a", "b"] and back.loc["b", "is_valid"] == False  # noqa: E712
     db.save_generation_info({"experiment_id": "e", "generation": 0})
     assert db.get_generations_count() == 1
-    db.save_resume_state(0, {"x": 1})
-    assert db.get_resume_state(0) == {"x": 1}
+    nxt = pd.DataFrame({"genotype": [np.zeros(4)], "parent_id": ["a"]}, index=pd.Index(["c"], name="id"))
+    db.save_resume_state(0, {"next_generation": nxt, "pool_size": 3, "rng": None})
+    st = db.get_resume_state(0)
+    assert st["pool_size"] == 3 and list(st["next_generation"].index) == ["c"] and "rng" not in st
+    assert db.get_resume_state(1) is None
