@@ -149,7 +149,7 @@ def test_fit_remainder_batch_matches_torch():
             if n.op != "bn":
                 continue
             for k in ("moving_mean", "moving_variance"):
-                want = org.params[f"n{n.id}_{k}"].detach().cpu().numpy()
+                want = org.p(n.id, k).detach().cpu().numpy()
                 base = np.zeros_like(want) if k == "moving_mean" else np.ones_like(want)
                 # compare the accumulated update (the statistics start at 0 / 1)
                 err = _rel(got[n.id][k] - base, want - base)
