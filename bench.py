@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--pop-per-gpu", type=int, default=125)
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--parameters", default=None)
+    ap.add_argument("--dump-population", default=None,
+                    help="write the source codes of the last generation (JSON list) for scripts/bench_step.py")
     ap.add_argument("--profile-dir", default=None,
                     help="torch.profiler Chrome trace of the run per rank (diagnostics; not a headline timing)")
     args = ap.parse_args()
@@ -116,6 +118,13 @@ def main():
             "generations": timed,
         }
         print(json.dumps(out), flush=True)
+    if comm.is_root and args.dump_population and db is not None:
+        import sqlite3
+        con = sqlite3.connect(db.db_path)
+        rows = con.execute("select source_code from serann where generation = (select max(generation) from serann)"
+                           " and is_valid = 1 and is_overweight = 0").fetchall()
+        with open(args.dump_population, "w") as f:
+            json.dump([r[0] for r in rows], f)
     comm.shutdown()
 
 

@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--out", default="gpurun_out/bench_kernels.json")
     ap.add_argument("--only", type=str, default="", help="comma-separated launch indices to time (profiling)")
+    ap.add_argument("--population-file", default=None, help="JSON list of source codes (bench.py --dump-population)")
     ap.add_argument("--ancestor-frac", type=float, default=0.0,
                     help="fraction of clones of the example.json ancestor (table codec): the bench's regime")
     a = ap.parse_args()
@@ -88,6 +89,9 @@ def main():
             irs.append(r.ir)
         if len(irs) == a.pop:
             break
+    if a.population_file:
+        with open(a.population_file) as f:
+            irs = [try_interpret(s).ir for s in json.load(f)][:a.pop]
     if a.ancestor_frac > 0:
         from serann.config import default_parameters
         from serann.experiment.runner import build_codec

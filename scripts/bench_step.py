@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--ancestor-frac", type=float, default=0.0,
                     help="fraction of the population that are clones of the example.json ancestor (table codec), "
                          "as in the bench's evolved generations")
+    ap.add_argument("--population-file", default=None,
+                    help="JSON list of source codes (bench.py --dump-population): the bench's evolved population")
     a = ap.parse_args()
     from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
     from serann.engine.base import TrainConfig
@@ -40,6 +42,10 @@ def main():
             irs.append(r.ir)
         if len(irs) == a.pop:
             break
+    if a.population_file:
+        import json
+        with open(a.population_file) as f:
+            irs = [try_interpret(s).ir for s in json.load(f)][:a.pop]
     if a.ancestor_frac > 0:
         from serann.config import default_parameters
         from serann.experiment.runner import build_codec

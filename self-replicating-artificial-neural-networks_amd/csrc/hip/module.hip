@@ -18,6 +18,7 @@ static py::dict desc_sizes() {
     d["TransDesc"] = 5 * sizeof(int64_t);
     d["ImcolDesc"] = sizeof(ImcolDesc);
     d["SplitFinDesc"] = sizeof(SplitFinDesc);
+    d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
     return d;
 }
 
@@ -38,6 +39,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("act_bwd", &launch_act_bwd);
     m.def("bn", &launch_bn);
     m.def("pool", &launch_pool);
+    m.def("convpool", &launch_convpool);
     m.def("copy2d", &launch_copy2d);
     m.def("loss", &launch_loss);
     m.def("popstats", &launch_popstats);

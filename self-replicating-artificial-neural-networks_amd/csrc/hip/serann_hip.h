@@ -83,6 +83,13 @@ struct BnDesc {
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
 struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
 struct SplitFinDesc { int64_t ws, out, bias, M, N, S, act, flags; };      // flags: 1 = fp32 output
+// Fused first-layer Conv2D + MaxPool2D on a raw single-channel image (convpool.hip).  w: bf16 [F][KH*KW];
+// bias / dw / dbias: fp32 (0 = none); y / dy: bf16 pooled [B][POH][POW][F]; idx: u8 argmax window offset.
+struct ConvPoolDesc {
+    int64_t x, w, bias, y, idx, dy, dw, dbias;
+    int64_t B, H, W, F, KH, KW, SH, SW, OH, OW, PH, PW, PSH, PSW, POH, POW, act, flags;
+};
+void launch_convpool(int backward, int kt, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;

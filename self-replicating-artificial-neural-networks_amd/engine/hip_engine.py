@@ -41,6 +41,37 @@ SLACK = 64  # elements of zeroed tail on every arena
 # v2: first direct-fragment version; v1: LDS-tiled version.  Kept selectable for A/B measurements.
 FUSE_BN_STATS = os.environ.get("SERANN_FUSE_BN_STATS", "1") != "0"
 GEMM_IMPL = os.environ.get("SERANN_GEMM", "v3")
+FUSE_CONVPOOL = os.environ.get("SERANN_FUSE_CONVPOOL", "1") != "0"
+
+
+def convpool_pairs(ir: OrganismIR) -> Dict[int, int]:
+    """Conv2D nodes on the raw single-channel image whose only consumer is a MaxPool2D: conv id -> pool
+    id.  Such a pair runs as one fused kernel (csrc/hip/convpool.hip) and the conv output -- and its
+    gradient -- is never materialised (SERANN_FUSE_CONVPOOL=0 turns it off)."""
+    if not FUSE_CONVPOOL or GEMM_IMPL != "v3":
+        return {}
+    consumers: Dict[int, List[int]] = {}
+    for n in ir.nodes:
+        for i in n.inputs:
+            consumers.setdefault(i, []).append(n.id)
+    out = {}
+    for n in ir.nodes:
+        if n.op != "gemm" or n.attrs["kind"] != "conv2d":
+            continue
+        a = n.attrs
+        src = ir.node(n.inputs[0])
+        if src.op != "input" or a["cin"] != 1 or a["act"] not in H.ACT_CODES:
+            continue
+        cons = consumers.get(n.id, [])
+        if len(cons) != 1 or ir.node(cons[0]).op != "pool" or ir.cls_head == n.id:
+            continue
+        pa = ir.node(cons[0]).attrs
+        if pa["c"] != a["f"] or pa["h"] != a["oh"] or pa["w"] != a["ow"]:
+            continue
+        if not H.convpool_ok(a["h"], a["w"], a["kh"], a["kw"]):
+            continue
+        out[n.id] = cons[0]
+    return out
 
 
 def _padded_zeros(shape, dtype, device) -> torch.Tensor:
@@ -156,6 +187,8 @@ class Plan:
                 L.bn(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "pool":
                 L.pool(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "convpool":
+                L.convpool(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "copy":
                 L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "splitfin":
@@ -352,7 +385,10 @@ class HipPopulationEngine(PopulationEngine):
                     bmap[n.id] = ("f32", f32.alloc(B * (NC + L)))
                     continue
                 bmap[n.id] = ("act", act.alloc(size))
-            rec = {"owner": owner, "act": bmap, "grad": {}, "idx": {}, "bn": {}}
+            fused_convs = set(convpool_pairs(ir))
+            for cid in fused_convs:
+                bmap.pop(cid, None)          # conv output never materialised (fused conv + pool)
+            rec = {"owner": owner, "act": bmap, "grad": {}, "idx": {}, "bn": {}, "fused_convs": fused_convs}
             for n in ir.nodes:
                 if n.op == "pool":
                     rec["idx"][n.id] = u8.alloc(B * math.prod(n.shape))
@@ -363,6 +399,8 @@ class HipPopulationEngine(PopulationEngine):
                 req = self._requires_grad(ir)
                 for n in ir.nodes:
                     if n.op in ("input", "reshape") or (n.op == "gemm" and n.attrs["kind"] == "head_rep"):
+                        continue
+                    if n.id in fused_convs:
                         continue
                     if n.op == "gemm" and n.attrs["kind"] == "head_cls":
                         NC, L = ir.num_classes, ir.genotype_size
@@ -627,6 +665,35 @@ class HipPopulationEngine(PopulationEngine):
         plan.imcol_lookup = raw_conv_imcol
 
         fcat, fcons = self._fused_concats(mem, org_iter)
+        cpool = [dict() for _ in range(P)]            # pool id -> fused conv id
+        for o, lay in org_iter():
+            cpool[o] = {pid: cid for cid, pid in convpool_pairs(lay.ir).items()}
+
+        def convpool_row(o, pool_node, conv_id):
+            lay_ = self.layouts[o]
+            rec_ = mem["orgs"][o]
+            c = lay_.ir.node(conv_id).attrs
+            pa = pool_node.attrs
+            src_ = lay_.ir.node(lay_.ir.node(conv_id).inputs[0]).attrs["name"]
+            return dict(x=inputs[o][src_], w=wptr_bf(lay_.w[conv_id]),
+                        bias=pptr(lay_.b[conv_id]) if conv_id in lay_.b else 0,
+                        y=self._act_ptr(mem, o, pool_node.id, inputs), idx=mem["u8"].ptr(rec_["idx"][pool_node.id]),
+                        dy=mem["grad"].ptr(rec_["grad"][pool_node.id]) if train else 0,
+                        dw=gptr(lay_.w[conv_id]) if train else 0,
+                        dbias=gptr(lay_.b[conv_id]) if train and conv_id in lay_.b else 0,
+                        B=B, H=c["h"], W=c["w"], F=c["f"], KH=c["kh"], KW=c["kw"], SH=c["sh"], SW=c["sw"],
+                        OH=c["oh"], OW=c["ow"], PH=pa["ph"], PW=pa["pw"], PSH=pa["sh"], PSW=pa["sw"],
+                        POH=pa["oh"], POW=pa["ow"], act=H.ACT_CODES[c["act"]], flags=0,
+                        _kt=H.convpool_variant(c["kh"], c["kw"], c["f"]))
+
+        def add_convpool(rows, backward):
+            by_kt: Dict[int, list] = {}
+            for r in rows:
+                by_kt.setdefault(r.pop("_kt"), []).append(r)
+            for kt in sorted(by_kt):
+                rws = by_kt[kt]
+                add_chunked("convpool", (1 if backward else 0, kt), rws, H.CONVPOOL_DTYPE,
+                            [H.convpool_chunks(r["B"], r["F"], backward) for r in rws], 1)
         # gemm node -> the (first) last-axis BatchNormalization reading its output with matching channels
         bn_consumer = [dict() for _ in range(P)]
         bn_prefused = set()
@@ -657,6 +724,7 @@ class HipPopulationEngine(PopulationEngine):
             p_rows, p_cnt = [], []
             bn_rows, bn_cnt, bn_cnt_st, bn_stat = [], [], [], []
             c_rows, c_cnt = [], []
+            cp_rows = []
             fallbacks = []
             for o, lay in org_iter():
                 ir = lay.ir
@@ -665,6 +733,11 @@ class HipPopulationEngine(PopulationEngine):
                     if depth_of[o][n.id] != d or n.op in ("input", "reshape"):
                         continue
                     a = n.attrs
+                    if n.id in rec["fused_convs"]:
+                        continue                      # computed by the fused conv + pool kernel
+                    if n.op == "pool" and n.id in cpool[o]:
+                        cp_rows.append(convpool_row(o, n, cpool[o][n.id]))
+                        continue
                     if n.op == "gemm":
                         if a["kind"] == "head_rep":
                             continue
@@ -762,6 +835,7 @@ class HipPopulationEngine(PopulationEngine):
                         fallbacks.append((o, n))
             add_gemm(H.MODE_FWD, g_rows, g_dims, extra_fin=fin_rows)
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
+            add_convpool(cp_rows, False)
             if bn_rows:
                 if train:
                     need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)
@@ -840,6 +914,7 @@ class HipPopulationEngine(PopulationEngine):
             ab_rows, ab_cnt = [], []
             wg_rows, wg_dims = [], []
             bn_red, bn_red_cnt = [], []
+            cpw_rows = []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             fb = []
             for o, lay in org_iter():
@@ -851,7 +926,11 @@ class HipPopulationEngine(PopulationEngine):
                     if n.op == "gemm" and n.attrs["kind"] == "head_rep":
                         continue
                     a = n.attrs
-                    if not rec["req"].get(n.id, False):
+                    if not rec["req"].get(n.id, False) or n.id in rec["fused_convs"]:
+                        continue
+                    if n.op == "pool" and n.id in cpool[o]:
+                        # fused pool backward + conv WGRAD + bias gradient (no DGRAD: raw image input)
+                        cpw_rows.append(convpool_row(o, n, cpool[o][n.id]))
                         continue
                     if n.op == "gemm":
                         head = a["kind"] == "head_cls"
@@ -977,6 +1056,7 @@ class HipPopulationEngine(PopulationEngine):
                         fb.append((o, n))
             add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, 1)
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
+            add_convpool(cpw_rows, True)
             if bn_red:
                 add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
             for stage in STAGES:

@@ -29,6 +29,10 @@ POOL_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "idx", "dy", "dx", "B", "H", 
 COPY_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "rows", "cols", "src_stride", "dst_stride", "flags"]])
 SPLITFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "bias", "M", "N", "S", "act", "flags"]])
 SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kernel
+CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy", "dw", "dbias", "B", "H", "W", "F",
+                                             "KH", "KW", "SH", "SW", "OH", "OW", "PH", "PW", "PSH", "PSW", "POH",
+                                             "POW", "act", "flags"]])
+CONVPOOL_FWD_IMGS, CONVPOOL_WGRAD_IMGS, CONVPOOL_MAXPIX = 16, 32, 1024   # convpool.hip
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
@@ -102,6 +106,27 @@ def pool_units(elements: int, channels: int) -> int:
     return int(elements) // (8 if int(channels) % 8 == 0 else 1)
 
 
+def convpool_kt(kh: int, kw: int) -> int:
+    """32-tap k steps of a fused conv+pool problem (convpool.hip instantiations 1..3)."""
+    return -(-int(kh) * int(kw) // 32)
+
+
+def convpool_variant(kh: int, kw: int, filters: int) -> int:
+    """Kernel instantiation of a fused conv+pool problem: k steps * 8 + 16-filter tiles per block."""
+    return convpool_kt(kh, kw) * 8 + min(4, -(-int(filters) // 16))
+
+
+def convpool_ok(h: int, w: int, kh: int, kw: int) -> bool:
+    """Shapes the fused first-layer Conv2D + MaxPool2D kernels accept (convpool.hip limits)."""
+    return int(h) * int(w) <= CONVPOOL_MAXPIX and 1 <= convpool_kt(kh, kw) <= 3
+
+
+def convpool_chunks(batch: int, filters: int, backward: bool) -> int:
+    """Blocks of one fused conv+pool problem: image chunks x groups of 64 filters."""
+    per = CONVPOOL_WGRAD_IMGS if backward else CONVPOOL_FWD_IMGS
+    return -(-int(batch) // per) * -(-int(filters) // 64)
+
+
 def red_chunks(rows: int, channels: int) -> int:
     """Blocks needed by a BN / act_bwd problem of shape [rows][channels]."""
     per = max(1, RED_ELEMS // max(int(channels), 1))
@@ -127,7 +152,8 @@ def check_layouts():
     sizes = lib().desc_sizes()
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
-                     ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE)]:
+                     ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
+                     ("ConvPoolDesc", CONVPOOL_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 

@@ -64,4 +64,33 @@ ARCHS = {
         "g_layer = Conv1D(filters=3, kernel_size=1)(g_layer)\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
         "con = Dense(units=24, activation='relu')(con)\nloss_balance = 0.5"),
+    # fused first-layer Conv2D + MaxPool2D (csrc/hip/convpool.hip): the bench's dominant clone ...
+    "convpool_bench_a": (
+        "X_layer=Conv2D(filters=32,kernel_size=5,strides=1)(X_layer)\nX_layer=MaxPool2D(pool_size=3)(X_layer)\n"
+        "g_layer=Conv1D(filters=32,kernel_size=5,strides=1)(g_layer)\ng_layer=Dense(units=51,activation='relu')(g_layer)\n"
+        "g_layer=BatchNormalization()(g_layer)\n"
+        "con=concatenate([Reshape((1,-1))(X_layer),Reshape((1,-1))(g_layer)])\n"
+        "con=Dense(units=135,activation='relu')(con)\nloss_balance=0.1329"),
+    # ... overlapping windows, relu on the conv, a partial 16-filter tile, 2 k steps of taps
+    "convpool_relu_overlap": (
+        "X_layer = Conv2D(filters=40, kernel_size=7, strides=2, activation='relu')(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=3, strides=2)(X_layer)\n\n"
+        "g_layer = Dense(units=24, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=64, activation='relu')(con)\n\nloss_balance = 0.6"),
+    # ... 9x9 taps (3 k steps), 80 filters (two 64-filter groups), a Dense after the pool
+    "convpool_k9_f80": (
+        "X_layer = Conv2D(filters=80, kernel_size=9, strides=1)(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=4)(X_layer)\n"
+        "X_layer = Dense(units=12, activation='relu')(X_layer)\n\n"
+        "g_layer = Dense(units=8, activation='sigmoid')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=32, activation='relu')(con)\n\nloss_balance = 0.5"),
+    # ... sigmoid conv, pool stride larger than the window (gaps)
+    "convpool_sigmoid_gap": (
+        "X_layer = Conv2D(filters=16, kernel_size=3, strides=1, activation='sigmoid')(X_layer)\n"
+        "X_layer = MaxPool2D(pool_size=2, strides=3)(X_layer)\n\n"
+        "g_layer = Dense(units=16, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.7"),
 }

@@ -30,7 +30,7 @@ def _batch(B, seed=0):
 
 
 def _oracle(ir, params, x, g, y):
-    dev = "cuda"
+    dev = "cpu"          # fp32 oracle on the CPU: independent of the GPU library paths
     org = Organism(ir, params, device=dev)
     xb = torch.as_tensor(x, device=dev)
     gb = torch.as_tensor(g, device=dev)
@@ -139,7 +139,7 @@ def test_fit_remainder_batch_matches_torch():
     hip = HipPopulationEngine(irs, seeds, device="cuda", cfg=cfg,
                               params=[init_params(ir, s) for ir, s in zip(irs, seeds)])
     rh = hip.fit(data, cfg)
-    ref = TorchPopulationEngine(irs, seeds, device="cuda", cfg=cfg)
+    ref = TorchPopulationEngine(irs, seeds, device="cpu", cfg=cfg)
     rr = ref.fit(data, cfg)
     assert rh.steps == rr.steps == 4
     for i, ir in enumerate(irs):
@@ -155,6 +155,40 @@ def test_fit_remainder_batch_matches_torch():
                 err = _rel(got[n.id][k] - base, want - base)
                 assert err < 0.1, (names[i], n.id, k, err)
     assert np.allclose(rh.train_acc, rr.train_acc, atol=0.05), (rh.train_acc, rr.train_acc)
+
+
+@pytest.mark.parametrize("name", [n for n in sorted(ARCHS) if n.startswith("convpool") or n == "conv_pool_dense"])
+def test_convpool_fusion_matches_unfused(name, monkeypatch):
+    """Fused first-layer Conv2D + MaxPool2D (one kernel each way, no conv output tensor) against the
+    unfused conv GEMM + pool kernels on the same parameters and batch: logits, every gradient (the conv
+    weights and bias included), and the pooled activations' argmax-routed gradient."""
+    from serann.engine import hip_engine as he
+    ir = interpret(ARCHS[name])
+    assert he.convpool_pairs(ir), name
+    params = init_params(ir, 5)
+    x, g, y = _batch(80, seed=4)
+    fused = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, mf = fused.debug_train_step(x, g, y)
+    lf = fused.debug_logits()[0]
+    monkeypatch.setattr(he, "FUSE_CONVPOOL", False)
+    assert not he.convpool_pairs(ir)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, mp = plain.debug_train_step(x, g, y)
+    lp = plain.debug_logits()[0]
+    assert _rel(lf, lp) < 2e-2, _rel(lf, lp)
+    # a sigmoid conv output stored in bf16 (unfused path: ~0.5 +- small, 2^-9 resolution) has many exact
+    # ties inside a pool window, broken towards the first position; the fused kernel takes the max of
+    # the fp32 pre-activations, so a few windows route their gradient elsewhere (both are exact argmaxes
+    # of their inputs; the fused path also matches the fp32 oracle, test_train_step_matches_oracle)
+    tol = 0.1 if "sigmoid" in name else 5e-2
+    a, b = fused.export_arena(0, gf), plain.export_arena(0, gp)
+    for nid in b:
+        for k in b[nid]:
+            if k.startswith("moving"):
+                continue
+            err = _rel(a[nid][k], b[nid][k])
+            assert err < tol or np.linalg.norm(b[nid][k]) < 5e-3, (name, nid, k, err)
+    assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
 
 
 def test_adam_kernel_matches_keras_formula():

@@ -15,6 +15,24 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+# fp32 PyTorch references run on the CPU: exact fp32 convolution math, independent of the GPU
+# library paths (MIOpen solver selection) the kernels under test are compared against
+def _cpu(t):
+    return t.detach().float().cpu() if torch.is_tensor(t) else t
+
+
+def ref_conv2d(x, w, b, stride):
+    return F.conv2d(_cpu(x), _cpu(w), _cpu(b), stride).to(DEV)
+
+
+def ref_conv2d_input(shape, w, dz, stride):
+    return torch.nn.grad.conv2d_input(shape, _cpu(w), _cpu(dz), stride).to(DEV)
+
+
+def ref_conv2d_weight(x, wshape, dz, stride):
+    return torch.nn.grad.conv2d_weight(_cpu(x), wshape, _cpu(dz), stride).to(DEV)
+
+
 def _rel(a, b):
     a, b = a.double(), b.double()
     return float((a - b).norm() / b.norm().clamp_min(1e-12))
@@ -99,7 +117,7 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     dz = torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16()
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)            # (F, C, KH, KW)
-    ref = F.conv2d(xr, wr, bias, (SH, SW)).permute(0, 2, 3, 1)
+    ref = ref_conv2d(xr, wr, bias, (SH, SW)).permute(0, 2, 3, 1)
     ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](ref)
     # FWD
     y = torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV)
@@ -112,7 +130,7 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     assert _rel(y.float(), ref) < 6e-3
     # DGRAD
     dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
-    ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    ref_dx = ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     flags = (H.GF_VEC_A if Fo % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
     wt = w.permute(3, 1, 2, 0).contiguous()       # Wt[C][KH][KW][F] for the v2 DGRAD kernel
     _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=(w if impl == "v1" else wt).data_ptr(), out=dx.data_ptr(),
@@ -121,7 +139,7 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     assert _rel(dx.float(), ref_dx) < 6e-3
     # WGRAD (accumulates into a zeroed fp32 buffer, split-K)
     dw = torch.zeros(Fo, KH, KW, C, device=DEV)
-    ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    ref_dw = ref_conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
                                   flags=flags, **geo)], [(Fo, K, B * OH * OW)], impl)
     assert _rel(dw, ref_dw) < 2e-5
@@ -226,7 +244,7 @@ def test_grouped_gemm_many_problems_one_launch(impl):
                          KW=KW, SH=SH, SW=SW, M=B * OH * OW, N=Fo, K=K, act=0,
                          flags=(H.GF_VEC_A if C % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)))
         dims.append((B * OH * OW, Fo, K))
-        refs.append(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, (SH, SW)).permute(0, 2, 3, 1))
+        refs.append(ref_conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, (SH, SW)).permute(0, 2, 3, 1))
         outs.append(y)
     _run_gemm(H.MODE_FWD, rows, dims, impl)
     for y, r in zip(outs, refs):
@@ -359,7 +377,7 @@ def test_fused_act_grad_and_bias_grad(act, impl, shape):
               [(Fo, K, B * OH * OW)], impl)
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)
-    ref_dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    ref_dw = ref_conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dw, ref_dw) < 1e-3
     assert _rel(db, dz.sum((0, 1, 2))) < 1e-3
     dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
@@ -367,7 +385,7 @@ def test_fused_act_grad_and_bias_grad(act, impl, shape):
     _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), aux=y.data_ptr(),
                                   act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
               [(B * Hh * Ww, C, KH * KW * Fo)], impl)
-    ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    ref_dx = ref_conv2d_input(xr.shape, wr, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref_dx) < 6e-3
 
 
@@ -407,11 +425,11 @@ def test_v3_accumulating_outputs(shape):
     wt = w.permute(3, 1, 2, 0).contiguous()
     _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
                                   K=KH * KW * Fo, flags=H.GF_ACCUM, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)], "v3")
-    ref = prev.float() + torch.nn.grad.conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
+    ref = prev.float() + ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref) < 6e-3
     prev_y = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
     y = prev_y.clone()
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), M=B * OH * OW, N=Fo,
                                 K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)], "v3")
-    ref_y = prev_y.float() + F.conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)
+    ref_y = prev_y.float() + ref_conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(y.float(), ref_y) < 6e-3
