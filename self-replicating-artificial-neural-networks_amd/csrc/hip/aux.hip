@@ -178,7 +178,8 @@ __device__ __forceinline__ float wsum(const float* ws, int C, int idx) {
     return v;
 }
 
-__device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, float* sA, float* sB) {
+template <int phase>
+__device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, float* sB) {
     const int R = (int)d.R, C = (int)d.C;
     const int flags = (int)d.flags;
     const float eps = (float)d.eps;
@@ -203,6 +204,49 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
 #pragma unroll
         for (int j = 0; j < 8; ++j) { ch[j] = c; c = (c + 1 == C) ? 0 : c + 1; }
     }
+    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
+    bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
+    bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
+    const bool skip_dx = phase == 5 && (flags & 8);
+    const bool acc_dx = phase == 5 && (flags & 4);
+
+    // Data loads are software-pipelined one batch of U super-rows ahead, and the first batch is issued
+    // BEFORE the per-channel parameter setup (whose workspace reads are a dependent chain of global
+    // loads): the block pays the parameter latency and the data latency once, overlapped.
+    constexpr int U = 4;
+    union V8 { uint4 u; bf16_t h[8]; };
+    struct Batch { V8 xv[U], gv[U], old[U]; int64_t e[U]; int nv[U]; };
+    auto issue = [&](Batch& bt, int sr) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int s_ = sr + k * G;
+            bt.e[k] = (int64_t)s_ * 8 * C + 8 * i;
+            bt.nv[k] = (active && s_ < sr1) ? (int)max((int64_t)0, min((int64_t)8, total - bt.e[k])) : 0;
+            bt.xv[k].u = make_uint4(0, 0, 0, 0);
+            bt.gv[k].u = make_uint4(0, 0, 0, 0);
+            bt.old[k].u = make_uint4(0, 0, 0, 0);
+            if (bt.nv[k] == 8) {
+                bt.xv[k].u = *reinterpret_cast<const uint4*>(x + bt.e[k]);
+                if (phase >= 4) bt.gv[k].u = *reinterpret_cast<const uint4*>(dy + bt.e[k]);
+                if (acc_dx) bt.old[k].u = *reinterpret_cast<const uint4*>(dx + bt.e[k]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {           // static indices: stays in registers
+                    if (j < bt.nv[k]) {
+                        bt.xv[k].h[j] = x[bt.e[k] + j];
+                        if (phase >= 4) bt.gv[k].h[j] = dy[bt.e[k] + j];
+                        if (acc_dx) bt.old[k].h[j] = dx[bt.e[k] + j];
+                    }
+                }
+            }
+        }
+    };
+    // phase 5 streams three tensors: a second batch in registers costs it occupancy (measured slower),
+    // so it only issues its first batch early and loads later batches in the loop
+    constexpr bool kAhead = phase != 5;
+    Batch cur, nxt;
+    if (!skip_dx) issue(cur, sr0 + q);
+
     // per-channel parameters into LDS (sA: scale-like, sB: shift-like)
     for (int c = t; c < C; c += 256) {
         float a = 0.f, b = 0.f;
@@ -271,60 +315,32 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     }
     __syncthreads();
     const bool reduce = phase == 0 || phase == 4;
-    if (phase == 5 && (flags & 8)) return;
+    if (skip_dx) return;
     float acc0[8], acc1[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { acc0[j] = 0.f; acc1[j] = 0.f; }
-    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
-    bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
-    bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
     if (active) {
-        // 4 super-rows per iteration: all loads are issued before any use (memory-level parallelism)
-        constexpr int U = 4;
         for (int sr = sr0 + q; sr < sr1; sr += U * G) {
-            union V8 { uint4 u; bf16_t h[8]; };
-            V8 xv[U], gv[U], old[U];
-            int64_t e[U];
-            int nv[U];
+            const bool more = sr + U * G < sr1;
+            if (!kAhead && sr != sr0 + q) issue(cur, sr);
+            if (kAhead && more) issue(nxt, sr + U * G);
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                const int s_ = sr + k * G;
-                e[k] = (int64_t)s_ * 8 * C + 8 * i;
-                nv[k] = s_ < sr1 ? (int)max((int64_t)0, min((int64_t)8, total - e[k])) : 0;
-                xv[k].u = make_uint4(0, 0, 0, 0);
-                gv[k].u = make_uint4(0, 0, 0, 0);
-                old[k].u = make_uint4(0, 0, 0, 0);
-                if (nv[k] == 8) {
-                    xv[k].u = *reinterpret_cast<const uint4*>(x + e[k]);
-                    if (phase >= 4) gv[k].u = *reinterpret_cast<const uint4*>(dy + e[k]);
-                    if (phase == 5 && (flags & 4)) old[k].u = *reinterpret_cast<const uint4*>(dx + e[k]);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {           // static indices: stays in registers
-                        if (j < nv[k]) {
-                            xv[k].h[j] = x[e[k] + j];
-                            if (phase >= 4) gv[k].h[j] = dy[e[k] + j];
-                            if (phase == 5 && (flags & 4)) old[k].h[j] = dx[e[k] + j];
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (nv[k] <= 0) continue;
+                const int nvk = cur.nv[k];
+                if (nvk <= 0) continue;
                 V8 ov;
                 if (phase == 0) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if (j < nv[k]) { const float v = bf2f(xv[k].h[j]) - pa[j]; acc0[j] += v; acc1[j] += v * v; }
+                        if (j < nvk) { const float v = bf2f(cur.xv[k].h[j]) - pa[j]; acc0[j] += v; acc1[j] += v * v; }
                     continue;
                 }
                 if (phase == 4) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        const float g = bf2f(gv[k].h[j]);
+                        const float g = bf2f(cur.gv[k].h[j]);
                         acc0[j] += g;
-                        acc1[j] += g * (bf2f(xv[k].h[j]) - pa[j]) * pb[j];
+                        acc1[j] += g * (bf2f(cur.xv[k].h[j]) - pa[j]) * pb[j];
                     }
                     continue;
                 }
@@ -332,19 +348,21 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
                 if (phase == 5) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        ov.h[j] = f2bf(pa[j] * bf2f(gv[k].h[j]) + pb[j] * bf2f(xv[k].h[j]) + p3[j] + bf2f(old[k].h[j]));
+                        ov.h[j] = f2bf(pa[j] * bf2f(cur.gv[k].h[j]) + pb[j] * bf2f(cur.xv[k].h[j]) + p3[j] +
+                                       bf2f(cur.old[k].h[j]));
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) ov.h[j] = f2bf(bf2f(xv[k].h[j]) * pa[j] + pb[j]);
+                    for (int j = 0; j < 8; ++j) ov.h[j] = f2bf(bf2f(cur.xv[k].h[j]) * pa[j] + pb[j]);
                 }
-                if (nv[k] == 8) {
-                    *reinterpret_cast<uint4*>(dst + e[k]) = ov.u;
+                if (nvk == 8) {
+                    *reinterpret_cast<uint4*>(dst + cur.e[k]) = ov.u;
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if (j < nv[k]) dst[e[k] + j] = ov.h[j];
+                        if (j < nvk) dst[cur.e[k] + j] = ov.h[j];
                 }
             }
+            if (kAhead && more) cur = nxt;
         }
     }
     if (reduce) {
@@ -391,14 +409,16 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, int phase, flo
     }
 }
 
-__global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ descs, const int2* __restrict__ tiles,
-                                                 int phase) {
+// One instantiation per phase: each keeps only the registers its phase uses (the software-pipelined
+// load batches of phase 5 hold x, dy and the accumulated dx; phases 0 / 2 / 3 only x).
+template <int phase>
+__global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ descs, const int2* __restrict__ tiles) {
     __shared__ float s0[4096];           // vectorised path: 2 x (G * 8 * C <= 2048) reduction slots
     __shared__ float s1[256];
     const int2 td = tiles[blockIdx.x];
     const BnDesc& d = descs[td.x];
     if (d.C <= 256) {
-        bn_vec(d, td.y, phase, s0, s1);
+        bn_vec<phase>(d, td.y, s0, s1);
         return;
     }
     const int R = (int)d.R, C = (int)d.C;
@@ -797,8 +817,18 @@ void launch_act_bwd(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t str
 
 void launch_bn(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
-    hipLaunchKernelGGL(bn_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
-                       as_ptr<const BnDesc>(descs), as_ptr<const int2>(tiles), phase);
+    const dim3 grid((unsigned)ntiles), block(256);
+    const BnDesc* dp = as_ptr<const BnDesc>(descs);
+    const int2* tp = as_ptr<const int2>(tiles);
+    hipStream_t s = as_stream(stream);
+    switch (phase) {
+        case 0: hipLaunchKernelGGL(bn_kernel<0>, grid, block, 0, s, dp, tp); break;
+        case 2: hipLaunchKernelGGL(bn_kernel<2>, grid, block, 0, s, dp, tp); break;
+        case 3: hipLaunchKernelGGL(bn_kernel<3>, grid, block, 0, s, dp, tp); break;
+        case 4: hipLaunchKernelGGL(bn_kernel<4>, grid, block, 0, s, dp, tp); break;
+        case 5: hipLaunchKernelGGL(bn_kernel<5>, grid, block, 0, s, dp, tp); break;
+        default: throw std::runtime_error("bn: bad phase");
+    }
     SERANN_CHECK(hipGetLastError());
 }
 

@@ -504,18 +504,19 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     // BNK = 16 (layers with <= 16 reduction columns, e.g. Dense on the raw image): the 4 waves split f
     // waves along f (a 128/256-row f tile covering a whole merged-Dense layer was measured 20 % slower
     // per step than 64-row tiles despite reading X once: fewer, heavier blocks)
-    constexpr int WR = (BNK == 16) ? 4 : ((BMF == 64) ? 2 : 1);
+    constexpr int WR = (BNK == 16) ? 4 : ((BMF >= 64) ? 2 : 1);
     constexpr int WC = 4 / WR;                       // waves along k
     constexpr int TF = BMF / WR / 16;
     constexpr int TK = BNK / WC / 16;
     const int wf = wave / WC, wk = wave % WC;
 
-    // A loader: rows m (64) x f (BMF) in chunks of 8 f
+    // A loader: rows m (64) x f (BMF) in chunks of 8 f (BMF = 160 / 192: 20 / 24 chunks per row, the
+    // threads past ACH * AROWS idle)
     constexpr int ACH = BMF / 8;
     constexpr int AROWS = 256 / ACH;                 // rows per pass
     constexpr int APASS = (BKM + AROWS - 1) / AROWS;
     const int a_f = (t % ACH) * 8, a_r = t / ACH;
-    const bool a_act = a_r < BKM;
+    const bool a_act = a_r < BKM && t < ACH * AROWS;
     const int a_nv = min(8, g.F - (f0 + a_f));       // valid f of this chunk (may be <= 0)
     // B loader: rows m (64) x k (BNK) in chunks of 8 k; the k chunk is fixed per thread
     constexpr int BCH = BNK / 8;
@@ -649,12 +650,19 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     }
 
     if (do_bias) {
-        // lanes of one wave holding the same f chunk differ in the bits >= log2(ACH)
+        if ((ACH & (ACH - 1)) == 0) {
+            // lanes of one wave holding the same f chunk differ in the bits >= log2(ACH)
 #pragma unroll
-        for (int xo = ACH; xo < 64; xo <<= 1)
+            for (int xo = ACH; xo < 64; xo <<= 1)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
-        if (a_act && lane < ACH) {
+                for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
+            if (a_act && lane < ACH) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+            }
+        } else if (a_act) {
+            // non-power-of-two chunk count (BMF = 160 / 192): one atomic per thread and f
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
@@ -1549,7 +1557,9 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
 // LDS-tiled GEMM for 1x1 / Dense problems (row-major A[M][K] with row stride C, B[N][K]):
 //   FWD   : Y = act(A . B^T + bias)          A = layer input,  B = Wm
 //   DGRAD : dX (+)= (dY * act'(Y)) . B^T     A = dY (+ Y),     B = Wt
-// Block tile 128 x BN (BN = 64 or 128) x 32, 4 waves in a 2 x 2 layout (64 x BN/2 each).  Both
+// Block tile 128 x BN (BN = 64, 128, 160 or 192: one n tile covers a merged Dense of up to 192 units, so
+// its input panel is read once and no half-empty second tile is computed) x 32, 4 waves in a 2 x 2
+// layout (64 x BN/2 each).  Both
 // operand tiles go through LDS, so the weight tile is fetched once per block instead of once per
 // wave (the direct-fragment kernel re-reads B in every wave), and the next k-step's global loads are in
 // flight while the current step multiplies (register-staged double buffer, one barrier per step).
@@ -1595,10 +1605,11 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 
     // loaders: thread t -> (row t/4 + 64 i, k chunk (t % 4) * 8)
     const int lr = t >> 2, lk = (t & 3) * 8;
-    constexpr int BPT = BN / 64;                     // B chunks per thread
+    constexpr int BPT = (BN + 63) / 64;              // B chunks per thread (BN = 160 / 192: the last partial)
     // BT loader: thread t -> (k row t / NCH + BKP i, n chunk (t % NCH) * 8)
-    constexpr int NCH = BN / 8, BKP = 256 / NCH, BTP = BK / BKP;
+    constexpr int NCH = BN / 8, BKP = 256 / NCH, BTP = (BK + BKP - 1) / BKP;
     const int bkr = t / NCH, bnc = (t % NCH) * 8;
+    const bool bt_act = t < NCH * BKP;
     uint4 ra[2], rb[BT ? BTP : BPT];
     auto gload = [&](int kt) {
         const int k = kt * BK + lk;
@@ -1617,7 +1628,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             for (int i = 0; i < BTP; ++i) {
                 const int kk = kt * BK + bkr + BKP * i;
                 const int n = n0 + bnc;
-                const int off = (kk < K && n < N) ? kk * ldb + n : -1;
+                const int off = (bt_act && bkr + BKP * i < BK && kk < K && n < N) ? kk * ldb + n : -1;
                 uint4 v = bl16(rB, off);
                 if (N - n < 8) v = splice(v, zero, N - n);
                 rb[i] = v;
@@ -1626,7 +1637,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
             for (int i = 0; i < BPT; ++i) {
                 const int n = n0 + lr + 64 * i;
-                const int off = (n < N && run > 0) ? n * ldb + k : -1;
+                const int off = (lr + 64 * i < BN && n < N && run > 0) ? n * ldb + k : -1;
                 uint4 v = bl16(rB, off);
                 if (run < 8) v = splice(v, zero, run);
                 rb[i] = v;
@@ -1640,11 +1651,12 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         if (BT) {
 #pragma unroll
             for (int i = 0; i < BTP; ++i)
-                *reinterpret_cast<uint4*>(&Bs[(buf * BK + bkr + BKP * i) * LDBT + bnc]) = rb[i];
+                if (bt_act && bkr + BKP * i < BK)
+                    *reinterpret_cast<uint4*>(&Bs[(buf * BK + bkr + BKP * i) * LDBT + bnc]) = rb[i];
         } else {
 #pragma unroll
             for (int i = 0; i < BPT; ++i)
-                *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
+                if (lr + 64 * i < BN) *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
         }
     };
 
@@ -1821,12 +1833,12 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,
 //                 or 5000 + NT + 10 * RT for the single-k-step (K <= 32) form, 6000 + K for narrow (K <= 4; + 100 staged, + 200 super-row),
-//                 7064 / 7128 for the LDS-tiled 1x1 kernel (BN = 64 / 128; tiles (prob, m tile, n tile, k range)),
-//                 8064 / 8128 the same for DGRAD with B = natural-layout weights [F][C] (BT)
+//                 7000 + BN for the LDS-tiled 1x1 kernel (BN = 64 / 128 / 160 / 192; tiles (prob, m tile, n tile,
+//                 k range)), 8000 + BN the same for DGRAD with B = natural-layout weights [F][C] (BT)
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
-// variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {64, 128, 256}
+// variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64, 128, 160}, BNK in {64, 128, 256}
 //                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, + 200: super-row form; F % 8 != 0);
 //                 tiles (prob, row block, 0, 0)
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
@@ -1873,6 +1885,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
+        W3(128, 128) W3(160, 128) W3(128, 64) W3(160, 64)
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
     }
@@ -1890,17 +1903,23 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef C3
         throw std::runtime_error("gemm3: unknown conv variant " + std::to_string(variant));
     }
-    if (variant == 7064 || variant == 7128) {
-        if (mode == MODE_FWD && variant == 7064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, 64>), grid, block, 0, s, dp, tp);
-        else if (mode == MODE_FWD) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, 128>), grid, block, 0, s, dp, tp);
-        else if (variant == 7064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 64>), grid, block, 0, s, dp, tp);
-        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128>), grid, block, 0, s, dp, tp);
+    if (variant == 7064 || variant == 7128 || variant == 7160 || variant == 7192) {
+#define TL(BN_)                                                                                     \
+    if (variant == 7000 + BN_) {                                                                    \
+        if (mode == MODE_FWD) hipLaunchKernelGGL((g3_tiled_kernel<MODE_FWD, BN_>), grid, block, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_>), grid, block, 0, s, dp, tp);      \
+    }
+        TL(64) TL(128) TL(160) TL(192)
+#undef TL
         SERANN_CHECK(hipGetLastError());
         return;
     }
-    if (mode == MODE_DGRAD && (variant == 8064 || variant == 8128)) {   // BT: natural-layout weights
+    if (mode == MODE_DGRAD && (variant == 8064 || variant == 8128 || variant == 8160 || variant == 8192)) {
+        // BT: natural-layout weights
         if (variant == 8064) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 64, true>), grid, block, 0, s, dp, tp);
-        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128, true>), grid, block, 0, s, dp, tp);
+        else if (variant == 8128) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 128, true>), grid, block, 0, s, dp, tp);
+        else if (variant == 8160) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 160, true>), grid, block, 0, s, dp, tp);
+        else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 192, true>), grid, block, 0, s, dp, tp);
         SERANN_CHECK(hipGetLastError());
         return;
     }

@@ -196,6 +196,13 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     im2col_gen = KW * C < 8 and W != KW and KH > 1
     if mode == MODE_WGRAD:
         bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
+        if 64 < M <= 160 and N > 16 and _WGRAD_WIDE:
+            # one f tile per layer up to 160 units (merged Dense): the X panel is read once and no
+            # mostly-empty last f tile is computed (192-row tiles spill registers).  Opt-in: at one wave
+            # per SIMD (241-256 VGPRs) it measured slower than 64-row tiles on the bench population
+            # (1.51 -> 2.22 ms per step, profiles/r2_wide_ab.txt)
+            bmf = 128 if M <= 128 else 160
+            return bmf * 1000 + (128 if N > 64 else 64) + (1000000 if im2col_gen else 0)
         if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
             return 64 * 1000 + 16 + (1000000 if im2col_gen else 0)
 
@@ -218,9 +225,9 @@ def gemm3_block(mode: int, variant: int):
     if mode == MODE_WGRAD:
         v = variant % 1000000
         return (v // 1000, v % 1000)
-    if variant in (7064, 7128):
+    if 7000 < variant < 7300:
         return (128, variant - 7000)
-    if variant in (8064, 8128):
+    if 8000 < variant < 8300:
         return (128, variant - 8000)
     if variant >= 5000:
         return (64 * ((variant // 10) % 10), 16 * (variant % 10))
@@ -298,6 +305,20 @@ def narrow_k(geo: dict, mode: int, M: int, N: int, K: int):
     return None
 
 
+TILED_BNS = (64, 128, 160, 192)               # gemm3.hip g3_tiled_kernel instantiations
+
+
+def tiled_bn(N: int) -> int:
+    """Column tile of the LDS-tiled 1x1 / Dense kernel: the smallest instantiation covering N (one n tile
+    reads the A panel once), 128-column tiles beyond 192."""
+    if "wide" in _OFF:
+        return 128 if N > 64 else 64
+    for bn in TILED_BNS:
+        if N <= bn:
+            return bn
+    return 128
+
+
 def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     """Group the problems of one grouped launch by v3 kernel instantiation.
 
@@ -313,7 +334,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
         v = None
         nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) and not r.get("_nonarrow") else None
         if r.get("_force_tiled"):
-            v = 7128 if N > 64 else 7064          # K slice of a concat input: LDS-tiled + workspace
+            v = 7000 + tiled_bn(N)                # K slice of a concat input: LDS-tiled + workspace
         elif nk is not None:
             # + 100: LDS-staged rows when the narrow kernel's row width (N, or F for WGRAD) is not a
             # multiple of 8 (unaligned 16-B row chunks); measured faster for K <= 2 (Dense on the raw
@@ -325,7 +346,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             v = (6000 if mode == MODE_FWD else 4000000) + nk + (200 if sr else 100 if st else 0)
         elif (mode in (MODE_FWD, MODE_DGRAD) and "tiled" not in _OFF and K > 32
               and int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1):
-            v = 7128 if N > 64 else 7064          # LDS-tiled 1x1 / Dense GEMM
+            v = 7000 + tiled_bn(N)                # LDS-tiled 1x1 / Dense GEMM
             if mode == MODE_DGRAD and r.get("_bnat") and "bt" not in _OFF:
                 # natural-layout weights read k-major (no transposed copy needed)
                 v += 1000
@@ -392,11 +413,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             dms = [dm for _, dm in items]
             if mode == MODE_WGRAD:
                 tg = [wgrad_target(M, N) for (M, N, K) in dms]
-                tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn)
+                tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
-            elif mode == MODE_FWD and v in (7064, 7128):
+            elif mode == MODE_FWD and 7000 < v < 7300:
                 tl = []
                 for p, (r, (M, N, K)) in enumerate(items):
                     kt = -(-K // BK)
@@ -406,6 +427,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                         r["kper"] = max(per, 1)
                         r["flags"] = int(r.get("flags", 0)) | GF_SPLITWS
                     t = gemm_tiles([(M, N, K)], mode, bm=bm, bn=bn)
+                    spl = []
                     for s_ in range(ns):
                         k0, k1 = s_ * per, min(kt, (s_ + 1) * per)
                         if k0 >= k1:
@@ -413,10 +435,13 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                         ts = t.copy()
                         ts[:, 0] = p
                         ts[:, 3] = k0 | (k1 << 16)
-                        tl.append(ts)
+                        spl.append(ts)
+                    # the m x n tiles of one k split share its X and W panels: one XCD per split
+                    if spl:
+                        tl.append(xcd_swizzle(np.concatenate(spl), len(t)))
                 tiles = np.concatenate(tl).astype(np.int32) if tl else np.zeros((0, 4), np.int32)
             else:
-                tiles = gemm_tiles(dms, mode, bm=bm, bn=bn)
+                tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000)
         out.append((v, [r for r, _ in items], tiles))
     return out
 
@@ -465,11 +490,12 @@ def wgrad_target(M: int, N: int) -> int:
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+_WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0") == "1"
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
 def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,
-               bn: int = BN) -> np.ndarray:
+               bn: int = BN, swizzle: bool = False) -> np.ndarray:
     """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16).
     target_ksteps: int, or one value per problem (WGRAD m-split granularity)."""
     rows = []
@@ -491,10 +517,38 @@ def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int
             packed = k0 | (k1 << 16)
             mm, nn = np.meshgrid(np.arange(tm), np.arange(tn), indexing="xy")
             blk = np.stack([np.full(tm * tn, p), mm.ravel(), nn.ravel(), np.full(tm * tn, packed)], 1)
+            if swizzle:
+                # m fastest: the tm tiles of one n column share its B panel (WGRAD: the X columns,
+                # DGRAD: the weight columns) -> keep them on one XCD
+                blk = xcd_swizzle(blk, tm)
             rows.append(blk)
     if not rows:
         return np.zeros((0, 4), np.int32)
     return np.concatenate(rows).astype(np.int32)
+
+
+XCDS = 8                                   # MI355X: 8 XCDs, blockIdx.x -> XCD blockIdx.x % 8 (round robin)
+XCD_SWIZZLE = "xcd" not in _OFF
+
+
+def xcd_swizzle(tiles: np.ndarray, group: int) -> np.ndarray:
+    """Reorder one problem's tile table so that every run of ``group`` consecutive tiles (tiles that
+    share an operand panel: the m tiles of one WGRAD column tile, the m x n tiles of one FWD k split)
+    is dispatched to ONE XCD, in consecutive rounds of the round-robin dispatch: their panel re-reads
+    hit that XCD's L2 instead of going to the Infinity Cache / HBM once per XCD.  Tiles are independent
+    (disjoint outputs or atomics), so the order is a pure performance choice; the tail that does not
+    fill 8 whole groups keeps its natural order."""
+    n = len(tiles)
+    g = int(group)
+    if not XCD_SWIZZLE or g <= 1 or n < XCDS * g:
+        return tiles
+    full = (n // (XCDS * g)) * XCDS * g
+    i = np.arange(full)
+    k, j = i // g, i % g
+    pos = ((k // XCDS) * g + j) * XCDS + (k % XCDS)
+    out = tiles.copy()
+    out[pos] = tiles[:full]
+    return out
 
 
 def chunk_tiles(counts, chunk: int) -> np.ndarray:
