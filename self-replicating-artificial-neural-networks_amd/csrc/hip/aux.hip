@@ -209,6 +209,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
     bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
     const bool skip_dx = phase == 5 && (flags & 8);
     const bool acc_dx = phase == 5 && (flags & 4);
+    const int pact = (flags >> 4) & 3;           // phase 5: fold the producer's act' into dx
 
     // Data loads are software-pipelined one batch of U super-rows ahead, and the first batch is issued
     // BEFORE the per-channel parameter setup (whose workspace reads are a dependent chain of global
@@ -347,9 +348,12 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
                 bf16_t* dst = (phase == 5) ? dx : y;
                 if (phase == 5) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        ov.h[j] = f2bf(pa[j] * bf2f(cur.gv[k].h[j]) + pb[j] * bf2f(cur.xv[k].h[j]) + p3[j] +
-                                       bf2f(cur.old[k].h[j]));
+                    for (int j = 0; j < 8; ++j) {
+                        const float xj = bf2f(cur.xv[k].h[j]);
+                        float v = pa[j] * bf2f(cur.gv[k].h[j]) + pb[j] * xj + p3[j] + bf2f(cur.old[k].h[j]);
+                        if (pact != ACT_LINEAR) v *= act_grad_from_y(xj, pact);
+                        ov.h[j] = f2bf(v);
+                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) ov.h[j] = f2bf(bf2f(cur.xv[k].h[j]) * pa[j] + pb[j]);
@@ -510,6 +514,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
                 const float xh = (bf2f(x[off]) - mu) * is;
                 float v = gg * (bf2f(dy[off]) - a - xh * b);
                 if (flags & 4) v += bf2f(dx[off]);
+                if ((flags >> 4) & 3) v *= act_grad_from_y(bf2f(x[off]), (int)((flags >> 4) & 3));
                 dx[off] = f2bf(v);
             }
         }

@@ -77,7 +77,9 @@ struct ActBwdDesc { int64_t dy, y, dz, dbias, M, N, act, flags; };          // f
 constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
-    int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx
+    int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx,
+                              // bits 4-5 (phase 5): act of the GEMM producing x -- dx is written as that
+                              // GEMM's dZ = dx * act'(x) (x is its output), so its backward reads no Y
     double eps, momentum;
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum

@@ -909,6 +909,30 @@ class HipPopulationEngine(PopulationEngine):
                     tcnt.append(-(-(F_ * P_ * C_) // H.TRANS_ELEMS))
             add_chunked("transpose", 0, trows, H.TRANS_DTYPE, tcnt, 1)
 
+        # BatchNormalization whose input is the output of an activated GEMM used by nothing else: its
+        # backward (phase 5) writes that GEMM's dZ = dx * act'(x) directly, so the GEMM's WGRAD / DGRAD
+        # read dZ alone instead of dY and Y (SERANN_FOLD_BN_ACT=0 turns it off)
+        dz_folded = [dict() for _ in range(P)]          # gemm id -> act code folded into the BN dx
+        if os.environ.get("SERANN_FOLD_BN_ACT", "1") != "0":
+            for o, lay in org_iter():
+                ir = lay.ir
+                rec = mem["orgs"][o]
+                owner = rec["owner"]
+                uses: Dict[int, int] = {}
+                for n in ir.nodes:
+                    if n.op == "reshape":
+                        continue
+                    for i in n.inputs:
+                        uses[owner.get(i, i)] = uses.get(owner.get(i, i), 0) + 1
+                for n in ir.nodes:
+                    if n.op != "bn" or not n.attrs["last"]:
+                        continue
+                    src = ir.node(owner[n.inputs[0]])
+                    if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
+                            and src.id not in rec["fused_convs"] and src.attrs["act"] in ("relu", "sigmoid")
+                            and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
+                        dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
+
         STAGES = ("dgrad", "pool", "bn", "copy")
         for d in range(maxd, 0, -1):
             ab_rows, ab_cnt = [], []
@@ -945,7 +969,8 @@ class HipPopulationEngine(PopulationEngine):
                             F, C = a["f"], a["cin"]
                             Hh, Ww, OH, OW = a["h"], a["w"], a["oh"], a["ow"]
                             KH, KW, SH, SW = a["kh"], a["kw"], a["sh"], a["sw"]
-                            act = H.ACT_CODES[a["act"]]
+                            # dZ already carries act' (written by the consuming BN's backward)
+                            act = 0 if n.id in dz_folded[o] else H.ACT_CODES[a["act"]]
                         M = B * OH * OW
                         K = KH * KW * C
                         dbias = gptr(lay.b[n.id]) if n.id in lay.b else 0
@@ -1029,6 +1054,8 @@ class HipPopulationEngine(PopulationEngine):
                                     R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
                         bn_red.append(dict(base, flags=pflags))
                         bn_red_cnt.append(H.bn_chunks(R, c, stats=True))
+                        if own is not None and own in dz_folded[o]:
+                            pflags |= dz_folded[o][own] << 4
                         if own is None:
                             tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
                                                 H.bn_chunks(R, c)))
