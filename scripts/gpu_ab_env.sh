@@ -6,11 +6,11 @@ out=gpurun_out/${1:-ab}
 mkdir -p $out
 export TMPDIR=/tmp
 step() { local name=$1 to=$2; shift 2; echo "=== $name"; timeout -k 10 "$to" "$@" > $out/$name.log 2>&1; local rc=$?; tail -3 $out/$name.log | cut -c1-300; [ $rc -eq 0 ] || { echo "$name failed rc=$rc"; tail -30 $out/$name.log; exit $rc; }; }
-P=profiles/r2_bench_population.json
-step step_a 250 python scripts/bench_step.py --population-file $P --streams 4
-step step_b 250 env $AB_ENV python scripts/bench_step.py --population-file $P --streams 4
-step kern_a 300 python scripts/bench_kernels.py --pop 125 --population-file $P --out $out/ka.json
-step kern_b 300 env $AB_ENV python scripts/bench_kernels.py --pop 125 --population-file $P --out $out/kb.json
+P=${POPFILE:-profiles/r2_bench_population.json}; [ "$P" = none ] && P=
+step step_a 250 python scripts/bench_step.py ${P:+--population-file $P} --streams 4
+step step_b 250 env $AB_ENV python scripts/bench_step.py ${P:+--population-file $P} --streams 4
+step kern_a 300 python scripts/bench_kernels.py --pop 125 ${P:+--population-file $P} --out $out/ka.json
+step kern_b 300 env $AB_ENV python scripts/bench_kernels.py --pop 125 ${P:+--population-file $P} --out $out/kb.json
 python - $out <<'PY'
 import json, sys
 o = sys.argv[1]
