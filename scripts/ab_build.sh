@@ -11,7 +11,7 @@ SUF=$(python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))
 PYI=$(python3 -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBI=$(python3 -c "import pybind11;print(pybind11.get_include())")
 for f in "$D"/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Wno-unused-result \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Wno-unused-result $ABFLAGS \
     -I"$D" -I"$PYI" -I"$PBI" -c "$f" -o "$SRC/$(basename "$f" .hip).o" &
 done
 wait

@@ -26,6 +26,9 @@
 #include "common.h"
 #include "serann_hip.h"
 
+#ifndef WG_NSETS
+#define WG_NSETS 2          // WGRAD register sets in flight (build-time A/B knob)
+#endif
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
@@ -480,10 +483,11 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
 // WGRAD: dWm[f][k] += sum_m dZ[m][f] * im2col(X)[m][k].  Tile BMF (f) x BNK (k), 64 rows of m per
 // step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
 // in LDS in that layout with 16-B writes; MFMA fragments come from ds_read_b64_tr_b16.
-template <int BMF, int BNK, bool GEN>
-__global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
+template <int BMF, int BNK, bool GEN, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                        const int4* __restrict__ tiles) {
     constexpr int BKM = 64;
+    constexpr int NTH = 64 * NWV;                    // threads per block (NWV = 8: wide f tiles, 2 x 4 waves)
     constexpr int LDA = BMF + 8, LDB = BNK + 8;
     __shared__ __attribute__((aligned(16))) bf16_t As[BKM * LDA];
     __shared__ __attribute__((aligned(16))) bf16_t Bs[BKM * LDB];
@@ -505,7 +509,7 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     // waves along f (a 128/256-row f tile covering a whole merged-Dense layer was measured 20 % slower
     // per step than 64-row tiles despite reading X once: fewer, heavier blocks)
     constexpr int WR = (BNK == 16) ? 4 : ((BMF >= 64) ? 2 : 1);
-    constexpr int WC = 4 / WR;                       // waves along k
+    constexpr int WC = NWV / WR;                     // waves along k
     constexpr int TF = BMF / WR / 16;
     constexpr int TK = BNK / WC / 16;
     const int wf = wave / WC, wk = wave % WC;
@@ -513,14 +517,14 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
     // A loader: rows m (64) x f (BMF) in chunks of 8 f (BMF = 160 / 192: 20 / 24 chunks per row, the
     // threads past ACH * AROWS idle)
     constexpr int ACH = BMF / 8;
-    constexpr int AROWS = 256 / ACH;                 // rows per pass
+    constexpr int AROWS = NTH / ACH;                 // rows per pass
     constexpr int APASS = (BKM + AROWS - 1) / AROWS;
     const int a_f = (t % ACH) * 8, a_r = t / ACH;
     const bool a_act = a_r < BKM && t < ACH * AROWS;
     const int a_nv = min(8, g.F - (f0 + a_f));       // valid f of this chunk (may be <= 0)
     // B loader: rows m (64) x k (BNK) in chunks of 8 k; the k chunk is fixed per thread
     constexpr int BCH = BNK / 8;
-    constexpr int BROWS = 256 / BCH;
+    constexpr int BROWS = NTH / BCH;
     constexpr int BPASS = (BKM + BROWS - 1) / BROWS;
     const int b_k = (t % BCH) * 8, b_r = t / BCH;
     const int kk = k0c + b_k;
@@ -630,7 +634,9 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
         }
     };
 
-    // kt counts 32-row units; one step consumes two of them (64 rows); steps alternate register sets
+    // kt counts 32-row units; one step consumes two of them (64 rows); steps rotate over WG_NSETS
+    // register sets, so the loads of a step are issued WG_NSETS steps before it is staged
+#if WG_NSETS == 2
     if (kt0 < kt1) load(kt0, ra0, rb0);
     if (kt0 + 2 < kt1) load(kt0 + 2, ra1, rb1);
     for (int kt = kt0; kt < kt1; kt += 4) {
@@ -648,6 +654,25 @@ __global__ __launch_bounds__(256) void g3_wgrad_kernel(const GemmDesc* __restric
         if (kt + 6 < kt1) load(kt + 6, ra1, rb1);
         compute();
     }
+#else
+    Frag rax[WG_NSETS][APASS], rbx[WG_NSETS][BPASS];
+#pragma unroll
+    for (int q_ = 0; q_ < WG_NSETS; ++q_)
+        if (kt0 + 2 * q_ < kt1) load(kt0 + 2 * q_, rax[q_], rbx[q_]);
+    for (int kt = kt0; kt < kt1; kt += 2 * WG_NSETS) {
+#pragma unroll
+        for (int q_ = 0; q_ < WG_NSETS; ++q_) {
+            const int kc = kt + 2 * q_;
+            if (kc >= kt1) break;
+            __syncthreads();
+            stash(rax[q_], rbx[q_]);
+            bias_acc(rax[q_]);
+            __syncthreads();
+            if (kc + 2 * WG_NSETS < kt1) load(kc + 2 * WG_NSETS, rax[q_], rbx[q_]);
+            compute();
+        }
+    }
+#endif
 
     if (do_bias) {
         if ((ACH & (ACH - 1)) == 0) {
@@ -1886,6 +1911,14 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
         W3(128, 128) W3(160, 128) W3(128, 64) W3(160, 64)
+#define W8(BMF_, BNK_) \
+    if (v == BMF_ * 1000 + BNK_ + 500) { \
+        const dim3 b8(512); \
+        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true, 8>), grid, b8, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 8>), grid, b8, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return; }
+        W8(128, 128) W8(160, 128) W8(128, 64) W8(160, 64) W8(192, 64)
+#undef W8
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
     }

@@ -196,11 +196,16 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     im2col_gen = KW * C < 8 and W != KW and KH > 1
     if mode == MODE_WGRAD:
         bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
-        if 64 < M <= 160 and N > 16 and _WGRAD_WIDE:
-            # one f tile per layer up to 160 units (merged Dense): the X panel is read once and no
-            # mostly-empty last f tile is computed (192-row tiles spill registers).  Opt-in: at one wave
-            # per SIMD (241-256 VGPRs) it measured slower than 64-row tiles on the bench population
-            # (1.51 -> 2.22 ms per step, profiles/r2_wide_ab.txt)
+        if 64 < M <= 192 and N > 16 and _WGRAD_WIDE == "8":
+            # one f tile per layer up to 192 units (merged Dense): the X panel is read once instead of
+            # once per 64-row f tile and no mostly-empty last f tile is computed; 8 waves per block (2 x 4)
+            # keep the per-thread accumulators and load registers at the 64-row tile's level (+500)
+            bmf = 128 if M <= 128 else (160 if M <= 160 else 192)
+            bnk = 128 if N > 64 and bmf < 192 else 64        # 192 x 128 spills registers
+            return bmf * 1000 + bnk + 500 + (1000000 if im2col_gen else 0)
+        if 64 < M <= 160 and N > 16 and _WGRAD_WIDE == "4":
+            # the same with 4 waves: at one wave per SIMD (241-256 VGPRs) it measured slower than 64-row
+            # tiles on the bench population (1.51 -> 2.22 ms per step, profiles/r2_wide_ab.txt)
             bmf = 128 if M <= 128 else 160
             return bmf * 1000 + (128 if N > 64 else 64) + (1000000 if im2col_gen else 0)
         if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
@@ -224,7 +229,7 @@ def gemm3_block(mode: int, variant: int):
     """(rows, cols) of the output tile one block of a v3 launch covers."""
     if mode == MODE_WGRAD:
         v = variant % 1000000
-        return (v // 1000, v % 1000)
+        return (v // 1000, (v % 1000) % 500)
     if 7000 < variant < 7300:
         return (128, variant - 7000)
     if 8000 < variant < 8300:
@@ -510,7 +515,7 @@ def wgrad_target(M: int, N: int) -> int:
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
-_WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0") == "1"
+_WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 

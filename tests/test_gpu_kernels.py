@@ -187,7 +187,7 @@ def test_tiled_fwd_split_k_with_finalize():
             H.lib().splitk_finalize(fd.data_ptr(), ft.data_ptr(), len(ft), H.stream_handle())
     torch.cuda.synchronize()
     assert nsplit >= 3
-    assert {v for v, _, _ in plans} >= {7160, 7192}
+    assert {v for v, _, _ in plans} & {7160, 7192}          # one shared wide width for the N > 64 group
     for y, r in zip(outs, refs):
         assert _rel(y.float(), r) < 6e-3
 
