@@ -1,0 +1,62 @@
+"""Host-side launch planning (no GPU): tile-table permutations, shared column widths, kernel variant
+selection and the fused conv + pool eligibility rules."""
+import numpy as np
+import pytest
+
+from serann.genome.interpreter import interpret
+from serann.ops import hip_ops as H
+
+from .archs import ARCHS
+
+
+@pytest.mark.parametrize("n,g", [(24, 3), (50, 3), (200, 6), (97, 12), (5, 2)])
+def test_xcd_swizzle_is_a_permutation_grouping_runs_on_one_xcd(n, g):
+    tiles = np.stack([np.arange(n)] * 4, 1).astype(np.int32)
+    out = H.xcd_swizzle(tiles, g)
+    assert sorted(out[:, 0].tolist()) == list(range(n))
+    full = (n // (H.XCDS * g)) * H.XCDS * g
+    pos = {int(t): i for i, t in enumerate(out[:, 0])}
+    for c in range(full // g):
+        assert len({pos[c * g + j] % H.XCDS for j in range(g)}) == 1
+    assert (out[full:] == tiles[full:]).all()                 # the tail keeps its natural order
+
+
+def _dense_rows(shapes):
+    return [dict(M=M, N=N, K=K, KH=1, KW=1, SH=1, SW=1, C=K, flags=0) for M, N, K in shapes]
+
+
+def test_tiled_widths_are_shared_per_launch_group():
+    shapes = [(750, 135, 784), (750, 110, 200), (750, 190, 500), (750, 40, 300)]
+    plans = H.gemm3_plan(H.MODE_FWD, _dense_rows(shapes), shapes)
+    widths = [v for v, _, _ in plans if 7000 < v < 7300]
+    assert 7064 in widths                                    # N <= 64 keeps its own narrow tile
+    assert len([w for w in widths if w != 7064]) == 1         # one width for every N > 64 problem
+    one = H.gemm3_plan(H.MODE_FWD, _dense_rows(shapes[:1]), shapes[:1])
+    assert [v for v, _, _ in one] == [7160]                    # N = 135 alone: one 160-column tile
+
+
+def test_wgrad_variants_default_to_64_row_tiles():
+    assert H.gemm3_variant(H.MODE_WGRAD, 135, 4896, 750, {}) == 64128
+    assert H.gemm3_block(H.MODE_WGRAD, 160628) == (160, 128)
+
+
+@pytest.mark.parametrize("name,fused", [("convpool_bench_a", True), ("convpool_k9_f80", True),
+                                        ("conv_pool_dense", True), ("odd_channels_bn", False),
+                                        ("conv1d_rank4_and_strided_pool", False), ("bn_first_and_pool3", False)])
+def test_convpool_eligibility(name, fused):
+    from serann.engine.hip_engine import convpool_pairs
+    ir = interpret(ARCHS[name])
+    pairs = convpool_pairs(ir)
+    assert bool(pairs) == fused
+    for cid, pid in pairs.items():
+        c, p = ir.node(cid), ir.node(pid)
+        assert c.attrs["cin"] == 1 and ir.node(c.inputs[0]).op == "input"
+        assert p.inputs == [cid] and H.convpool_ok(c.attrs["h"], c.attrs["w"], c.attrs["kh"], c.attrs["kw"])
+
+
+def test_convpool_variant_encoding():
+    assert H.convpool_variant(5, 5, 32) == 1 * 8 + 2
+    assert H.convpool_variant(7, 7, 40) == 2 * 8 + 3
+    assert H.convpool_variant(9, 9, 80) == 3 * 8 + 4
+    assert H.convpool_chunks(750, 80, backward=False) == -(-750 // H.CONVPOOL_FWD_IMGS) * 2
+    assert not H.convpool_ok(28, 28, 11, 11)                  # > 96 taps
