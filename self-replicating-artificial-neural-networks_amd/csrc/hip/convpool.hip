@@ -9,7 +9,8 @@
 // * FWD: per image, the block stages the 28x28 input in LDS and runs one bf16 MFMA per (window
 //   offset, 16 pooled positions, 16 filters): A = the patches of the conv positions at that window
 //   offset (gathered from LDS), B = the filter bank (registers).  The max over the window offsets is
-//   an element-wise max of accumulators in registers; bias + activation are applied after the max
+//   an element-wise max of accumulators in registers (window code packed into the low mantissa bits:
+//   2 VALU ops per conv output); bias + activation are applied after the max
 //   (both are monotone non-decreasing, so max(act(z + b)) = act(max(z) + b)) and the pooled output
 //   and the argmax window offset are the only stores.
 // * WGRAD: dW[f][tap] = sum_{b,p} dz[b,p,f] [argmax == w] img[b][pos(p, w) + tap], one MFMA per
@@ -95,15 +96,17 @@ struct CpStager {
     }
 };
 
-// Running max of one accumulator element over the window offsets: first maximum in (i, j) scan order
-// (strict >), 3 VALU ops.  NaN is tracked separately through a running sum (a NaN operand makes it
-// NaN), and a NaN window yields a NaN output, as the unfused pool kernel propagates NaN.
-__device__ __forceinline__ void cp_max(float v, int code, float& best, int& bi, float& nsum) {
-    const bool gt = v > best;
-    best = gt ? v : best;
-    bi = gt ? code : bi;
-    nsum += v;
+// Running max of one accumulator element over the window offsets in 2 VALU ops: the window code is
+// packed into the low 8 mantissa bits (255 - code, so that on a tie the first window in (i, j) scan order
+// wins for values >= 0) and the packed values are max-ed as floats.  The kept value is truncated by at
+// most 2^-15 relative before its bf16 rounding.  maxNum drops NaN: a NaN conv output can only come from
+// non-finite filter weights (the image is finite), which are flagged per filter instead (cp_nan).
+__device__ __forceinline__ float cp_key(float v, int code) {
+    return __uint_as_float((__float_as_uint(v) & 0xffffff00u) | (uint32_t)(255 - code));
 }
+__device__ __forceinline__ float cp_key_value(float key) { return __uint_as_float(__float_as_uint(key) & 0xffffff00u); }
+__device__ __forceinline__ int cp_key_code(float key) { return 255 - (int)(__float_as_uint(key) & 0xffu); }
+__device__ __forceinline__ bf16_t cp_bf16(float v) { return __builtin_bit_cast(bf16_t, (__bf16)v); }
 
 // KT: 32-tap k steps; NT: 16-filter tiles per block (<= 4); G: 16-position groups per pass (ILP)
 template <int KT, int NT>
@@ -151,10 +154,19 @@ __global__ __launch_bounds__(256) void convpool_fwd_kernel(const ConvPoolDesc* _
         }
     }
     float bv[NT];
+    bool cp_nan[NT];                                 // filter has a non-finite weight -> NaN outputs
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int f = f0 + nt * 16 + col;
         bv[nt] = (bias != nullptr && f < F) ? bias[f] : 0.f;
+        float sw = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sw += fabsf(bf2f(bw[kt][nt].h[j]));
+        sw += __shfl_xor(sw, 16, 64);
+        sw += __shfl_xor(sw, 32, 64);
+        cp_nan[nt] = !(sw <= 3.0e38f);
     }
 
     bf16_t* slot = img[wave];
@@ -176,14 +188,13 @@ __global__ __launch_bounds__(256) void convpool_fwd_kernel(const ConvPoolDesc* _
                 const int poh = pa / POW, pw_ = pa - poh * POW;
                 base[g] = poh * PSH * SH * W + pw_ * PSW * SW;
             }
-            float best[G][NT][4], nsum[G][NT][4];
-            int bi[G][NT][4];
+            float best[G][NT][4];                    // packed (value, 255 - window code) keys
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) { best[g][nt][r] = -INFINITY; bi[g][nt][r] = 0; nsum[g][nt][r] = 0.f; }
+                    for (int r = 0; r < 4; ++r) best[g][nt][r] = -3.0e38f;
             // window offsets in (i, j) scan order; the patches of window wi + 1 are read from LDS while
             // window wi runs its MFMAs and max updates (register double buffer)
             const int nwin = PH * PW;
@@ -228,7 +239,7 @@ __global__ __launch_bounds__(256) void convpool_fwd_kernel(const ConvPoolDesc* _
                         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
-                                cp_max(acc[g][nt][r], code, best[g][nt][r], bi[g][nt][r], nsum[g][nt][r]);
+                                best[g][nt][r] = fmaxf(best[g][nt][r], cp_key(acc[g][nt][r], code));
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g)
@@ -248,9 +259,10 @@ __global__ __launch_bounds__(256) void convpool_fwd_kernel(const ConvPoolDesc* _
                         const int p = pg + g * 16 + kg * 4 + r;
                         if (p >= npos) continue;
                         const int64_t o = ((int64_t)b * npos + p) * F + f;
-                        const float v = nsum[g][nt][r] != nsum[g][nt][r] ? nsum[g][nt][r] : best[g][nt][r];
-                        y[o] = f2bf(apply_act(v + bv[nt], act));
-                        if (idx != nullptr) idx[o] = (uint8_t)bi[g][nt][r];
+                        const float key = best[g][nt][r];
+                        const float v = cp_nan[nt] ? __builtin_nanf("") : cp_key_value(key);
+                        y[o] = cp_bf16(apply_act(v + bv[nt], act));
+                        if (idx != nullptr) idx[o] = (uint8_t)cp_key_code(key);
                     }
                 }
         }
