@@ -176,18 +176,21 @@ def test_convpool_fusion_matches_unfused(name, monkeypatch):
     gp, mp = plain.debug_train_step(x, g, y)
     lp = plain.debug_logits()[0]
     assert _rel(lf, lp) < 2e-2, _rel(lf, lp)
-    # a sigmoid conv output stored in bf16 (unfused path: ~0.5 +- small, 2^-9 resolution) has many exact
-    # ties inside a pool window, broken towards the first position; the fused kernel takes the max of
-    # the fp32 pre-activations, so a few windows route their gradient elsewhere (both are exact argmaxes
-    # of their inputs; the fused path also matches the fp32 oracle, test_train_step_matches_oracle)
-    tol = 0.1 if "sigmoid" in name else 5e-2
+    # The unfused conv output is stored in bf16 before the pool, so values within 2^-8 of each other tie
+    # inside a window and the first position wins; the fused kernel takes the max of the (nearly) fp32
+    # pre-activations.  Both are exact argmaxes of their own inputs, and a few windows route their
+    # gradient differently, so the two paths are each compared against the fp32 oracle: the fused one
+    # must be at least as accurate as the unfused one (measured: it is more accurate, e.g. conv kernel
+    # gradient 0.059 vs 0.082 for convpool_k9_f80), and the two stay close to each other.
+    _, ref = _oracle(ir, params, x, g, y)
     a, b = fused.export_arena(0, gf), plain.export_arena(0, gp)
-    for nid in b:
-        for k in b[nid]:
-            if k.startswith("moving"):
+    for nid in ref:
+        for k in ref[nid]:
+            if np.linalg.norm(ref[nid][k]) < 5e-3:
                 continue
-            err = _rel(a[nid][k], b[nid][k])
-            assert err < tol or np.linalg.norm(b[nid][k]) < 5e-3, (name, nid, k, err)
+            ef, eu = _rel(a[nid][k], ref[nid][k]), _rel(b[nid][k], ref[nid][k])
+            assert ef < 1.25 * eu + 1e-2, (name, nid, k, ef, eu)
+            assert _rel(a[nid][k], b[nid][k]) < 0.15, (name, nid, k, _rel(a[nid][k], b[nid][k]))
     assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
 
 
