@@ -23,7 +23,13 @@ def main():
     from serann.genome.generator import generate
     from serann.genome.interpreter import try_interpret
 
-    pop, frac = 125, float(sys.argv[1]) if len(sys.argv) > 1 else 0.8
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("frac", nargs="?", type=float, default=0.8)
+    ap.add_argument("--population-file", default=None,
+                    help="JSON list of source codes (bench.py --dump-population): the bench's evolved population")
+    a = ap.parse_args()
+    pop, frac = 125, a.frac
     df = generate(pop * 3, seed=11, validation_genotype_size=100)
     irs = [r.ir for r in (try_interpret(decoded_form(s)) for s in df["code"]) if r.ok and r.parameters_count <= 2e6][:pop]
     params = default_parameters("example")
@@ -31,6 +37,11 @@ def main():
     anc = try_interpret(codec.decode_to_string(np.asarray(params["ancestor_genotype"])[None])[0]).ir
     k = int(round(frac * pop))
     irs = [anc] * k + irs[:pop - k]
+    if a.population_file:
+        import json
+        with open(a.population_file) as f:
+            irs = [try_interpret(s).ir for s in json.load(f)][:pop]
+        pop = len(irs)
     data = get_serann_data(synthetic_encodings(), synthetic_mnist())
     cfg = TrainConfig(epochs=5, batch_size=750)
     for rep in range(2):

@@ -54,6 +54,11 @@ def _hipcc():
     raise FileNotFoundError("hipcc not found")
 
 
+# gchain.hip keeps its MFMA accumulators in VGPRs: they are read by VALU epilogues every tile, and the
+# AGPR form costs a v_accvgpr_read per element
+PER_FILE_FLAGS = {"gchain.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build_hip(jobs: int = 4):
     NATIVE.mkdir(exist_ok=True)
     build_dir = PKG / "_build"
@@ -68,10 +73,11 @@ def build_hip(jobs: int = 4):
 
     def compile_one(src):
         obj = build_dir / (src.stem + ".o")
+        extra = PER_FILE_FLAGS.get(src.name, [])
         # incremental: an object newer than its source and every header is reused
         if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_mtime):
             return obj
-        _run([hipcc, *flags, "-c", str(src), "-o", str(obj)])
+        _run([hipcc, *flags, *extra, "-c", str(src), "-o", str(obj)])
         return obj
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -19,6 +19,7 @@ static py::dict desc_sizes() {
     d["ImcolDesc"] = sizeof(ImcolDesc);
     d["SplitFinDesc"] = sizeof(SplitFinDesc);
     d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
+    d["GChainDesc"] = sizeof(GChainDesc);
     return d;
 }
 
@@ -40,6 +41,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("bn", &launch_bn);
     m.def("pool", &launch_pool);
     m.def("convpool", &launch_convpool);
+    m.def("gchain", &launch_gchain);
     m.def("copy2d", &launch_copy2d);
     m.def("loss", &launch_loss);
     m.def("popstats", &launch_popstats);

@@ -92,6 +92,18 @@ struct ConvPoolDesc {
     int64_t B, H, W, F, KH, KW, SH, SW, OH, OW, PH, PW, PSH, PSW, POH, POW, act, flags;
 };
 void launch_convpool(int backward, int kt, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+// Fused genotype-branch chain Conv1D(raw genotype) -> Dense -> [BatchNormalization] (gchain.hip).
+// g: bf16 [B][L0]; w1: bf16 [F1][T]; w2: bf16 [F2][F1]; biases / BN parameters / gradients fp32;
+// y, dy: bf16 [B * L1][F2] (the BN output when GC_BN, else the Dense output); rows per block rpb.
+struct GChainDesc {
+    int64_t g, w1, b1, w2, b2, y, dy, dw1, db1, dw2, db2;
+    int64_t gamma, beta, mm, mv, mean, invstd, ws, wsb, dgamma, dbeta;
+    int64_t B, L0, L1, T, S, F1, F2, act1, act2, flags, rpb;
+    int64_t dvL1;     // fast-division magic of L1 (hip_ops.fast_div_magic)
+    double eps, momentum;
+};
+enum GChainFlags : int64_t { GC_BN = 1, GC_GAMMA = 2, GC_BETA = 4, GC_TRAIN = 8 };
+void launch_gchain(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;

@@ -42,6 +42,7 @@ SLACK = 64  # elements of zeroed tail on every arena
 FUSE_BN_STATS = os.environ.get("SERANN_FUSE_BN_STATS", "1") != "0"
 GEMM_IMPL = os.environ.get("SERANN_GEMM", "v3")
 FUSE_CONVPOOL = os.environ.get("SERANN_FUSE_CONVPOOL", "1") != "0"
+FUSE_GCHAIN = os.environ.get("SERANN_FUSE_GCHAIN", "1") != "0"
 
 
 def convpool_pairs(ir: OrganismIR) -> Dict[int, int]:
@@ -71,6 +72,48 @@ def convpool_pairs(ir: OrganismIR) -> Dict[int, int]:
         if not H.convpool_ok(a["h"], a["w"], a["kh"], a["kw"]):
             continue
         out[n.id] = cons[0]
+    return out
+
+
+def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
+    """Replication-branch chains ``Conv1D(raw genotype) -> Dense -> [BatchNormalization]`` run by the
+    fused kernels of csrc/hip/gchain.hip: last node id -> (conv id, dense id, BN id or None).
+
+    Eligible: a Conv1D on the raw single-channel genotype whose only consumer is a Dense on its output
+    (<= 16 taps and a gchain_variant for the filter / unit counts); the BatchNormalization joins when it
+    is the Dense's only consumer and normalises its last axis.  The conv output -- and, with the BN, the
+    Dense output -- and their gradients are never materialised (SERANN_FUSE_GCHAIN=0 turns it off)."""
+    if not FUSE_GCHAIN or GEMM_IMPL != "v3":
+        return {}
+    consumers: Dict[int, List[int]] = {}
+    for n in ir.nodes:
+        for i in n.inputs:
+            consumers.setdefault(i, []).append(n.id)
+    out = {}
+    for n in ir.nodes:
+        if n.op != "gemm" or n.attrs["kind"] != "conv1d":
+            continue
+        a = n.attrs
+        src = ir.node(n.inputs[0])
+        if src.op != "input" or a["cin"] != 1 or a["w"] != 1 or a["kw"] != 1 or a["act"] not in H.ACT_CODES:
+            continue
+        cons = consumers.get(n.id, [])
+        if len(cons) != 1:
+            continue
+        dn = ir.node(cons[0])
+        if dn.op != "gemm" or dn.attrs["kind"] != "dense" or list(dn.inputs) != [n.id]:
+            continue
+        da = dn.attrs
+        if (da["cin"] != a["f"] or da["h"] != a["oh"] or da["w"] != 1 or da["act"] not in H.ACT_CODES
+                or H.gchain_variant(a["f"], da["f"], a["kh"]) is None):
+            continue
+        bn = None
+        dc = consumers.get(dn.id, [])
+        if len(dc) == 1:
+            b = ir.node(dc[0])
+            if b.op == "bn" and b.attrs["last"] and b.attrs["channels"] == da["f"]:
+                bn = b.id
+        out[bn if bn is not None else dn.id] = (n.id, dn.id, bn)
     return out
 
 
@@ -189,6 +232,8 @@ class Plan:
                 L.pool(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "convpool":
                 L.convpool(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "gchain":
+                L.gchain(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "copy":
                 L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "splitfin":
@@ -386,9 +431,18 @@ class HipPopulationEngine(PopulationEngine):
                     continue
                 bmap[n.id] = ("act", act.alloc(size))
             fused_convs = set(convpool_pairs(ir))
-            for cid in fused_convs:
-                bmap.pop(cid, None)          # conv output never materialised (fused conv + pool)
-            rec = {"owner": owner, "act": bmap, "grad": {}, "idx": {}, "bn": {}, "fused_convs": fused_convs}
+            gch = gchain_triples(ir)
+            no_tensor = set(fused_convs)     # outputs (and gradients) never materialised
+            gc_nodes = set()
+            for cid, did, bid in gch.values():
+                gc_nodes.update(i for i in (cid, did, bid) if i is not None)
+                no_tensor.add(cid)
+                if bid is not None:
+                    no_tensor.add(did)
+            for cid in no_tensor:
+                bmap.pop(cid, None)          # fused conv + pool, fused genotype chain
+            rec = {"owner": owner, "act": bmap, "grad": {}, "idx": {}, "bn": {}, "fused_convs": fused_convs,
+                   "gchain": gch, "gc_nodes": gc_nodes}
             for n in ir.nodes:
                 if n.op == "pool":
                     rec["idx"][n.id] = u8.alloc(B * math.prod(n.shape))
@@ -400,7 +454,7 @@ class HipPopulationEngine(PopulationEngine):
                 for n in ir.nodes:
                     if n.op in ("input", "reshape") or (n.op == "gemm" and n.attrs["kind"] == "head_rep"):
                         continue
-                    if n.id in fused_convs:
+                    if n.id in no_tensor:
                         continue
                     if n.op == "gemm" and n.attrs["kind"] == "head_cls":
                         NC, L = ir.num_classes, ir.genotype_size
@@ -694,13 +748,64 @@ class HipPopulationEngine(PopulationEngine):
                 rws = by_kt[kt]
                 add_chunked("convpool", (1 if backward else 0, kt), rws, H.CONVPOOL_DTYPE,
                             [H.convpool_chunks(r["B"], r["F"], backward) for r in rws], 1)
+        def gchain_row(o, last):
+            """Descriptor of the fused genotype chain ending at node ``last`` of organism ``o``."""
+            lay_ = self.layouts[o]
+            rec_ = mem["orgs"][o]
+            ir_ = lay_.ir
+            cid, did, bid = rec_["gchain"][last]
+            c = ir_.node(cid).attrs
+            dn = ir_.node(did).attrs
+            src_ = ir_.node(ir_.node(cid).inputs[0]).attrs["name"]
+            gl = rec_["grad"].get(last) if train else None
+            row = dict(g=inputs[o][src_], w1=wptr_bf(lay_.w[cid]), b1=pptr(lay_.b[cid]) if cid in lay_.b else 0,
+                       w2=wptr_bf(lay_.w[did]), b2=pptr(lay_.b[did]) if did in lay_.b else 0,
+                       y=self._act_ptr(mem, o, last, inputs), dy=mem["grad"].ptr(gl) if gl is not None else 0,
+                       dw1=gptr(lay_.w[cid]) if train else 0, db1=gptr(lay_.b[cid]) if train and cid in lay_.b else 0,
+                       dw2=gptr(lay_.w[did]) if train else 0, db2=gptr(lay_.b[did]) if train and did in lay_.b else 0,
+                       B=B, L0=c["h"], L1=c["oh"], T=c["kh"], S=c["sh"], F1=c["f"], F2=dn["f"],
+                       dvL1=H.fast_div_magic(c["oh"]),
+                       act1=H.ACT_CODES[c["act"]], act2=H.ACT_CODES[dn["act"]], flags=H.GC_TRAIN if train else 0,
+                       eps=1e-3, momentum=0.99, _bn=bid is not None,
+                       _v=H.gchain_variant(c["f"], dn["f"], c["kh"])
+                       + 64 * (3 * (c["act"] != "linear") + H.ACT_CODES[dn["act"]]))
+            if bid is not None:
+                bd = rec_["bn"][bid]
+                ba = ir_.node(bid).attrs
+                row.update(gamma=pptr(lay_.gamma[bid]) if bid in lay_.gamma else 0,
+                           beta=pptr(lay_.beta[bid]) if bid in lay_.beta else 0,
+                           mm=sptr(lay_.mm[bid]), mv=sptr(lay_.mv[bid]), mean=f32a.ptr(bd["mean"]),
+                           invstd=f32a.ptr(bd["invstd"]), ws=mem["ws"].ptr(bd["ws"]), wsb=mem["ws"].ptr(bd["wsb"]),
+                           dgamma=gptr(lay_.gamma[bid]) if train and bid in lay_.gamma else 0,
+                           dbeta=gptr(lay_.beta[bid]) if train and bid in lay_.beta else 0,
+                           eps=ba["epsilon"], momentum=ba["momentum"])
+                row["flags"] |= H.GC_BN | (H.GC_GAMMA if bid in lay_.gamma else 0) | (H.GC_BETA if bid in lay_.beta else 0)
+            return row
+
+        def add_gchain(rows, mode_):
+            """One launch per kernel instantiation; rows per block sized to the launch's grid."""
+            by_v: Dict[int, list] = {}
+            for r in rows:
+                by_v.setdefault(r["_v"], []).append(dict(r))
+            for v in sorted(by_v):
+                rws = by_v[v]
+                counts = []
+                for r in rws:
+                    R_ = int(r["B"]) * int(r["L1"])
+                    r["rpb"] = H.gchain_rpb(R_, len(rws), mode_, int(r["L1"]), int(r["L0"]))
+                    counts.append(-(-R_ // r["rpb"]))
+                tiles = H.chunk_tiles(counts, 1)
+                if len(tiles):
+                    plan.launches.append(Launch("gchain", (mode_, v), desc_tensor(rws, H.GCHAIN_DTYPE), T(tiles),
+                                                len(tiles)))
+
         # gemm node -> the (first) last-axis BatchNormalization reading its output with matching channels
         bn_consumer = [dict() for _ in range(P)]
         bn_prefused = set()
         for o, lay in org_iter():
             owner = mem["orgs"][o]["owner"]
             for n in lay.ir.nodes:
-                if n.op == "bn" and n.attrs["last"]:
+                if n.op == "bn" and n.attrs["last"] and n.id not in mem["orgs"][o]["gc_nodes"]:
                     src = lay.ir.node(owner[n.inputs[0]])
                     if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
                             and src.attrs["f"] == n.attrs["channels"] and src.id not in bn_consumer[o]):
@@ -725,6 +830,7 @@ class HipPopulationEngine(PopulationEngine):
             bn_rows, bn_cnt, bn_cnt_st, bn_stat = [], [], [], []
             c_rows, c_cnt = [], []
             cp_rows = []
+            gc_rows = []
             fallbacks = []
             for o, lay in org_iter():
                 ir = lay.ir
@@ -733,6 +839,10 @@ class HipPopulationEngine(PopulationEngine):
                     if depth_of[o][n.id] != d or n.op in ("input", "reshape"):
                         continue
                     a = n.attrs
+                    if n.id in rec["gc_nodes"]:
+                        if n.id in rec["gchain"]:
+                            gc_rows.append(gchain_row(o, n.id))   # the whole chain, at its last node's depth
+                        continue
                     if n.id in rec["fused_convs"]:
                         continue                      # computed by the fused conv + pool kernel
                     if n.op == "pool" and n.id in cpool[o]:
@@ -836,6 +946,9 @@ class HipPopulationEngine(PopulationEngine):
             add_gemm(H.MODE_FWD, g_rows, g_dims, extra_fin=fin_rows)
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             add_convpool(cp_rows, False)
+            if train:
+                add_gchain([r for r in gc_rows if r["_bn"]], H.GC_FSTAT)
+            add_gchain(gc_rows, H.GC_FAPPLY)
             if bn_rows:
                 if train:
                     need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)
@@ -892,6 +1005,8 @@ class HipPopulationEngine(PopulationEngine):
                 ir = lay.ir
                 for nid, off in lay.w.items():
                     a = ir.node(nid).attrs
+                    if nid in mem["orgs"][o]["gc_nodes"]:
+                        continue                      # fused genotype chain: no DGRAD launch
                     if a["kind"] == "head_cls":
                         F_, P_, C_ = ir.num_classes + ir.genotype_size, 1, ir.head_features
                     else:
@@ -925,7 +1040,7 @@ class HipPopulationEngine(PopulationEngine):
                     for i in n.inputs:
                         uses[owner.get(i, i)] = uses.get(owner.get(i, i), 0) + 1
                 for n in ir.nodes:
-                    if n.op != "bn" or not n.attrs["last"]:
+                    if n.op != "bn" or not n.attrs["last"] or n.id in rec["gc_nodes"]:
                         continue
                     src = ir.node(owner[n.inputs[0]])
                     if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
@@ -939,6 +1054,7 @@ class HipPopulationEngine(PopulationEngine):
             wg_rows, wg_dims = [], []
             bn_red, bn_red_cnt = [], []
             cpw_rows = []
+            gcb_rows = []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             fb = []
             for o, lay in org_iter():
@@ -950,6 +1066,10 @@ class HipPopulationEngine(PopulationEngine):
                     if n.op == "gemm" and n.attrs["kind"] == "head_rep":
                         continue
                     a = n.attrs
+                    if n.id in rec["gc_nodes"]:
+                        if n.id in rec["gchain"]:
+                            gcb_rows.append(gchain_row(o, n.id))
+                        continue
                     if not rec["req"].get(n.id, False) or n.id in rec["fused_convs"]:
                         continue
                     if n.op == "pool" and n.id in cpool[o]:
@@ -1084,6 +1204,8 @@ class HipPopulationEngine(PopulationEngine):
             add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, 1)
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             add_convpool(cpw_rows, True)
+            add_gchain([r for r in gcb_rows if r["_bn"]], H.GC_BSTAT)
+            add_gchain(gcb_rows, H.GC_BFULL)
             if bn_red:
                 add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
             for stage in STAGES:

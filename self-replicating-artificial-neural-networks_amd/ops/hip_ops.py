@@ -33,6 +33,12 @@ CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy",
                                              "KH", "KW", "SH", "SW", "OH", "OW", "PH", "PW", "PSH", "PSW", "POH",
                                              "POW", "act", "flags"]])
 CONVPOOL_FWD_IMGS, CONVPOOL_WGRAD_IMGS, CONVPOOL_MAXPIX = 16, 32, 1024   # convpool.hip
+GCHAIN_DTYPE = np.dtype([(f, _I) for f in ["g", "w1", "b1", "w2", "b2", "y", "dy", "dw1", "db1", "dw2", "db2",
+                                           "gamma", "beta", "mm", "mv", "mean", "invstd", "ws", "wsb", "dgamma",
+                                           "dbeta", "B", "L0", "L1", "T", "S", "F1", "F2", "act1", "act2", "flags",
+                                           "rpb", "dvL1"]] + [("eps", np.float64), ("momentum", np.float64)])
+GC_BN, GC_GAMMA, GC_BETA, GC_TRAIN = 1, 2, 4, 8          # gchain.hip GChainFlags
+GC_FSTAT, GC_FAPPLY, GC_BSTAT, GC_BFULL = 0, 1, 2, 3     # gchain.hip modes
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
@@ -121,6 +127,37 @@ def convpool_ok(h: int, w: int, kh: int, kw: int) -> bool:
     return int(h) * int(w) <= CONVPOOL_MAXPIX and 1 <= convpool_kt(kh, kw) <= 3
 
 
+def gchain_variant(f1: int, f2: int, taps: int):
+    """Instantiation (F1K * 8 + F2K) of the fused genotype chain for a Conv1D with ``f1`` filters and
+    ``taps`` taps followed by a Dense of ``f2`` units, or None when gchain.hip has none: T <= 16,
+    F1 <= 32 with F2 <= 128, or F1 <= 64 with F2 <= 64."""
+    f1k, f2k = -(-int(f1) // 32), -(-int(f2) // 32)
+    if not 1 <= int(taps) <= 16 or f1 < 1 or f2 < 1:
+        return None
+    if (f1k == 1 and f2k <= 4) or (f1k == 2 and f2k <= 2):
+        return f1k * 8 + f2k
+    return None
+
+
+GCHAIN_BLOCKS = {0: 4096, 1: 4096, 2: 8192, 3: 2048}     # target grid size per mode (gchain.hip)
+GCHAIN_GMAX = 8192                                        # gchain.hip GC_GMAX: staged genotype elements
+
+
+def gchain_rpb(rows: int, nprob: int, mode: int, l1: int = 1, l0: int = 0) -> int:
+    """Rows per block of a fused-chain launch over ``nprob`` problems of ``rows`` rows (conv output
+    length ``l1``, genotype length ``l0``): a multiple of 128 (4 waves x 32-row backward super-tiles)
+    sized so the grid reaches the mode's target block count (the full backward has fewer, longer
+    blocks: one fp32 atomic flush per gradient element and block), and small enough that the block's
+    genotype rows fit the LDS staging buffer."""
+    per = -(-int(rows) * max(1, int(nprob)) // GCHAIN_BLOCKS[int(mode)])
+    rpb = max(128, -(-per // 128) * 128)
+    rpb = min(rpb, -(-int(rows) // 128) * 128)
+    if l0 > 0:
+        while rpb > 64 and (-(-rpb // max(1, int(l1))) + 1) * int(l0) > GCHAIN_GMAX:
+            rpb -= 64
+    return rpb
+
+
 def convpool_chunks(batch: int, filters: int, backward: bool) -> int:
     """Blocks of one fused conv+pool problem: image chunks x groups of 64 filters."""
     per = CONVPOOL_WGRAD_IMGS if backward else CONVPOOL_FWD_IMGS
@@ -153,7 +190,7 @@ def check_layouts():
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
-                     ("ConvPoolDesc", CONVPOOL_DTYPE)]:
+                     ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 

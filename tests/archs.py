@@ -93,4 +93,34 @@ ARCHS = {
         "g_layer = Dense(units=16, activation='relu')(g_layer)\n\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
         "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.7"),
+    # fused genotype chains (csrc/hip/gchain.hip): Conv1D(raw genotype) -> Dense -> [BN] ...
+    "gchain_sigmoid_stride2": (
+        "X_layer = Dense(units=20, activation='relu')(X_layer)\n"
+        "g_layer = Conv1D(filters=16, kernel_size=3, strides=2)(g_layer)\n"
+        "g_layer = Dense(units=40, activation='sigmoid')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=32, activation='relu')(con)\n\nloss_balance = 0.4"),
+    # ... no BN, 9 taps, 100 units (4 k steps over the Dense output)
+    "gchain_nobn_k9_f100": (
+        "X_layer = MaxPool2D(pool_size=4)(X_layer)\n"
+        "g_layer = Conv1D(filters=8, kernel_size=9, strides=1)(g_layer)\n"
+        "g_layer = Dense(units=100, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=48, activation='relu')(con)\n\nloss_balance = 0.3"),
+    # ... 64 filters (two k steps into the Dense), 1 tap, a Dense after the BN (dy not from a concat)
+    "gchain_f64_bn_dense": (
+        "g_layer = Conv1D(filters=64, kernel_size=1, strides=1)(g_layer)\n"
+        "g_layer = Dense(units=64, activation='relu')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n"
+        "g_layer = Dense(units=10, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.6"),
+    # ... activated Conv1D, stride 3, Dense output read by two consumers (no BN fused, dy accumulated)
+    "gchain_relu_conv_fanout": (
+        "g_layer = Conv1D(filters=24, kernel_size=7, strides=3, activation='relu')(g_layer)\n"
+        "g_layer = Dense(units=20, activation='sigmoid')(g_layer)\n"
+        "X_layer = Dense(units=12, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=16, activation='relu')(con)\n\nloss_balance = 0.5"),
 }

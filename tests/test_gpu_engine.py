@@ -67,9 +67,12 @@ def test_train_step_matches_oracle(name):
                 # bf16 rounding noise of the HIP path remains -> absolute check
                 assert np.linalg.norm(got) < 2e-2, (name, nid, k, np.linalg.norm(got))
                 continue
-            err = _rel(got, v)
+            # a gradient that nearly cancels (|v| < 2 % of its layer's kernel gradient, e.g. the bias of a
+            # Conv1D under a sigmoid Dense + BatchNormalization) is judged on the layer's scale
+            scale = 0.02 * np.linalg.norm(d["kernel"]) if "kernel" in d else 0.0
+            err = np.linalg.norm(np.asarray(got, np.float64) - v) / max(np.linalg.norm(v), scale, 1e-12)
             cos = float(np.dot(got.ravel(), v.ravel()) / (np.linalg.norm(got) * np.linalg.norm(v) + 1e-30))
-            assert err < 0.2 and cos > 0.98, (name, nid, k, err, cos)
+            assert err < 0.2 and (cos > 0.98 or np.linalg.norm(v) < scale), (name, nid, k, err, cos)
     assert metrics[0, 3] == 96
 
 
@@ -192,6 +195,61 @@ def test_convpool_fusion_matches_unfused(name, monkeypatch):
             assert ef < 1.25 * eu + 1e-2, (name, nid, k, ef, eu)
             assert _rel(a[nid][k], b[nid][k]) < 0.15, (name, nid, k, _rel(a[nid][k], b[nid][k]))
     assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("name", [n for n in sorted(ARCHS) if n.startswith("gchain") or n == "convpool_bench_a"])
+def test_gchain_fusion_matches_unfused(name, monkeypatch):
+    """Fused genotype chain Conv1D(raw genotype) -> Dense -> [BatchNormalization] (gchain.hip: the chain
+    is recomputed from the genotype in every pass, no intermediate tensor) against the unfused GEMM / BN
+    kernels on the same parameters and batch: logits, every gradient against the fp32 oracle (the fused
+    path keeps the pre-BN activations in fp32, the unfused one in bf16), the BatchNorm moving
+    statistics, and inference logits through the moving statistics."""
+    from serann.engine import hip_engine as he
+    ir = interpret(ARCHS[name])
+    assert he.gchain_triples(ir), name
+    params = init_params(ir, 5)
+    x, g, y = _batch(80, seed=4)
+    fused = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, mf = fused.debug_train_step(x, g, y)
+    lf = fused.debug_logits()[0]
+    monkeypatch.setattr(he, "FUSE_GCHAIN", False)
+    assert not he.gchain_triples(ir)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, mp = plain.debug_train_step(x, g, y)
+    lp = plain.debug_logits()[0]
+    ref_logits, ref = _oracle(ir, params, x, g, y)
+    # (a sigmoid Dense's output stored in bf16 before the BN -- unfused -- is the less accurate one)
+    assert _rel(lf, ref_logits) < max(1.5 * _rel(lp, ref_logits), 1e-2), (_rel(lf, ref_logits), _rel(lp, ref_logits))
+    assert np.allclose(mf[:, 3], mp[:, 3])
+    a, b = fused.export_arena(0, gf), plain.export_arena(0, gp)
+    for nid in ref:
+        for k in ref[nid]:
+            if np.linalg.norm(ref[nid][k]) < 5e-3:
+                assert np.linalg.norm(a[nid][k]) < 2e-2, (name, nid, k, np.linalg.norm(a[nid][k]))
+                continue
+            r = np.asarray(ref[nid][k], np.float64)
+            ef, eu = np.linalg.norm(a[nid][k] - r), np.linalg.norm(b[nid][k] - r)
+            # relu / argmax boundary flips make either path the closer one by chance (measured rel. err.:
+            # gchain_f64_bn_dense fused 0.014-0.057 vs unfused 0.017-0.023, convpool_bench_a 0.03-0.12 vs
+            # 0.035-0.09 over two seeds; on sigmoid chains the fused path is 2-3x closer): a bound, not an
+            # ordering, inside the oracle test's 0.2.  Near-cancelling biases are bounded on their layer's scale.
+            kscale = np.linalg.norm(ref[nid]["kernel"]) if "kernel" in ref[nid] else 0.0
+            assert ef < max(1.5 * eu, 0.15 * max(np.linalg.norm(r), 0.2 * kscale)), (name, nid, k, ef, eu)
+    # moving statistics after one training step, then inference (moving statistics) through both paths
+    sf, sp = fused.export_params(0), plain.export_params(0)
+    for nid in sp:
+        for k in ("moving_mean", "moving_variance"):
+            if k in sp[nid]:
+                base = np.zeros_like(sp[nid][k]) if k == "moving_mean" else np.ones_like(sp[nid][k])
+                assert _rel(sf[nid][k] - base, sp[nid][k] - base) < 2e-2, (name, nid, k)
+    from serann.engine.base import TrainConfig
+    cfg = TrainConfig(batch_size=40)
+    labels = y.astype(np.int64)
+    monkeypatch.setattr(he, "FUSE_GCHAIN", True)
+    acc_f = fused.evaluate(x, labels, g, cfg)
+    monkeypatch.setattr(he, "FUSE_GCHAIN", False)
+    acc_p = plain.evaluate(x, labels, g, cfg)
+    assert np.allclose(acc_f, acc_p, atol=0.05), (acc_f, acc_p)
 
 
 def test_adam_kernel_matches_keras_formula():
