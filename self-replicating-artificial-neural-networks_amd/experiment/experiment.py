@@ -228,8 +228,8 @@ class Experiment:
     def _learn_and_replicate(self, current: pd.DataFrame, pool_size: int, generation: int):
         p = self._parameters
         sources = list(current["source_code"])
-        plan = plan_generation(sources, self._cache, float(p["max_serann_parameters"]))
         comm = self._comm
+        plan = plan_generation(sources, self._cache, float(p["max_serann_parameters"]), comm)
         parts = lpt_partition(plan.costs, comm.world_size, plan.arch_keys)
         local = [int(plan.trainable[i]) for i in parts[comm.rank]]
         ids = list(current.index)

@@ -55,7 +55,9 @@ class TableCodec(GeneticCodec):
         self.table = [decoded_form(s) for s in sources]
         self.genotype_size = genotype_size
         self.max_tokens = max_tokens
-        self.anchors = dict(anchors or {})
+        # anchors are stored in decoded form: the ancestor's unmutated clones are a large share of every
+        # early generation, and re-tokenising the source per clone cost ~2 ms each (pop 1000: ~1 s/gen)
+        self.anchors = {k: decoded_form(v) for k, v in (anchors or {}).items()}
         self.sensitive_bits = sensitive_bits or genotype_size
         self.salt = salt.encode()
         self.name = f"table{len(self.table)}"
@@ -92,7 +94,7 @@ class TableCodec(GeneticCodec):
         out = []
         for full, sens in zip(packed_full, packed_sens):
             a = self.anchors.get(full.tobytes())
-            out.append(decoded_form(a) if a is not None else self.table[self._index(sens.tobytes())])
+            out.append(a if a is not None else self.table[self._index(sens.tobytes())])
         return out
 
     # a table codec has no inverse: encoding returns the genotype of a table row when known

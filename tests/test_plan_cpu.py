@@ -60,3 +60,40 @@ def test_convpool_variant_encoding():
     assert H.convpool_variant(9, 9, 80) == 3 * 8 + 4
     assert H.convpool_chunks(750, 80, backward=False) == -(-750 // H.CONVPOOL_FWD_IMGS) * 2
     assert not H.convpool_ok(28, 28, 11, 11)                  # > 96 taps
+
+
+@pytest.mark.parametrize("name,expect", [
+    ("convpool_bench_a", "bn"), ("gchain_sigmoid_stride2", "bn"), ("gchain_f64_bn_dense", "bn"),
+    ("gchain_nobn_k9_f100", "dense"), ("gchain_relu_conv_fanout", "dense"), ("bn_first_and_pool3", "dense"),
+    ("odd_channels_bn", None), ("conv1d_rank4_and_strided_pool", None), ("narrow_bn_ancestor", None)])
+def test_gchain_eligibility(name, expect):
+    """Conv1D on the raw genotype whose only consumer is a Dense; the BatchNormalization joins only when
+    it is the Dense's sole consumer (a fan-out Dense output stays materialised)."""
+    from serann.engine.hip_engine import gchain_triples
+    ir = interpret(ARCHS[name])
+    tr = gchain_triples(ir)
+    if expect is None:
+        assert not tr
+        return
+    assert len(tr) == 1
+    last, (cid, did, bid) = next(iter(tr.items()))
+    c, dn = ir.node(cid), ir.node(did)
+    assert c.attrs["kind"] == "conv1d" and ir.node(c.inputs[0]).op == "input" and dn.inputs == [cid]
+    assert (bid is not None) == (expect == "bn")
+    assert last == (bid if bid is not None else did)
+    assert H.gchain_variant(c.attrs["f"], dn.attrs["f"], c.attrs["kh"]) is not None
+
+
+def test_gchain_variant_and_block_sizing():
+    assert H.gchain_variant(32, 51, 5) == 1 * 8 + 2
+    assert H.gchain_variant(8, 100, 9) == 1 * 8 + 4
+    assert H.gchain_variant(64, 64, 1) == 2 * 8 + 2
+    assert H.gchain_variant(64, 100, 1) is None          # F1 > 32 needs F2 <= 64
+    assert H.gchain_variant(16, 129, 3) is None          # F2 > 128
+    assert H.gchain_variant(16, 64, 17) is None          # > 16 taps
+    for mode in range(4):
+        for rows, l1, nprob in ((72000, 96, 112), (750, 1, 3), (8000, 100, 1), (363000, 484, 2)):
+            rpb = H.gchain_rpb(rows, nprob, mode, l1, 100)
+            assert rpb % 64 == 0 and rpb >= 64
+            # the block's genotype rows fit the kernel's LDS staging buffer
+            assert (-(-rpb // l1) + 1) * 100 <= H.GCHAIN_GMAX
