@@ -869,6 +869,10 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 // per-lane addresses into the patch, so every input element is fetched from global once per chunk
 // instead of KH*KW times.  Accumulators stay in registers across chunks; one fp32 atomic flush at the
 // end (the bias gradient is reduced by the k'-tile-0 blocks from the staged dZ rows).
+// Small outputs (OH*OW < 128, e.g. a 7x7 conv on an 11x11 map: 25 pixels) would leave most of a
+// 128-row chunk empty, so a chunk then covers ipc = min(128 / (OH*OW), PATCH / (H*W*Cs)) whole
+// consecutive images when ipc >= 2 (their input images are one contiguous NHWC range; hip_ops
+// conv_wgrad_ipc mirrors the rule for the tile table).
 template <int BMF, int BNK, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
@@ -888,6 +892,21 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const int Cs = (C8 & 1) ? Cp : Cp + 8;
     const int taps = g.KH * g.KW;
     const int nbatch = g.K / ohw;
+    const int hwcs = g.H * g.W * Cs;
+    const int ipc_full = ohw < TM ? min(TM / ohw, PATCH / hwcs) : 0;
+    const bool multi = ipc_full >= 2;            // chunk = ipc whole images
+    // chunk -> (first image, first pixel, last pixel of the chunk relative to that image's pixel 0)
+    auto chunk_geom = [&](int ch, int& b, int& m0, int& m_last) {
+        if (multi) {
+            b = ch * ipc_full;
+            m0 = 0;
+            m_last = min(ipc_full, nbatch - b) * ohw - 1;
+        } else {
+            b = ch / tpi;
+            m0 = (ch - b * tpi) * TM;
+            m_last = min(m0 + TM, ohw) - 1;
+        }
+    };
     const rsrc_t rX = mkrsrc(d.b, (int64_t)nbatch * g.H * g.W * g.C * 2);
     const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
@@ -940,13 +959,18 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     uint4 pre[PLD], apre[ALD];
     int cur_npix = 0;
     auto fetch = [&](int ch) {
-        const int b = ch / tpi;
-        const int m0 = (ch - b * tpi) * TM;
-        const int oh_a = fdiv(m0, g.dOW);
-        const int m_last = min(m0 + TM, ohw) - 1;
-        const int oh_b = fdiv(m_last, g.dOW);
-        const int npix = ((oh_b - oh_a) * g.SH + g.KH) * g.W;
-        const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
+        int b, m0, m_last;
+        chunk_geom(ch, b, m0, m_last);
+        int npix, gbase;
+        if (multi) {
+            npix = (m_last / ohw + 1) * g.H * g.W;       // whole images
+            gbase = b * g.H * g.W * g.C;
+        } else {
+            const int oh_a = fdiv(m0, g.dOW);
+            const int oh_b = fdiv(m_last, g.dOW);
+            npix = ((oh_b - oh_a) * g.SH + g.KH) * g.W;
+            gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
+        }
         cur_npix = npix;
 #pragma unroll
         for (int k = 0; k < PLD; ++k) {
@@ -979,10 +1003,9 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
 
     if (td.z < td.w) fetch(td.z);
     for (int ch = td.z; ch < td.w; ++ch) {
-        const int b = ch / tpi;
-        const int m0 = (ch - b * tpi) * TM;
-        const int oh_a = fdiv(m0, g.dOW);
-        const int m_last = min(m0 + TM, ohw) - 1;
+        int b, m0, m_last;
+        chunk_geom(ch, b, m0, m_last);
+        const int oh_a = multi ? 0 : fdiv(m0, g.dOW);
         const int npix = cur_npix;
         __syncthreads();                              // previous chunk's LDS reads are done
 #pragma unroll
@@ -1016,9 +1039,11 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             for (int h = 0; h < 2; ++h) {
                 int m = m0 + sub * 32 + grp * 8 + 4 * h + q;
                 if (m > m_last) m = m0;
-                const int oh = fdiv(m, g.dOW);
-                const int ow = m - oh * g.OW;
-                roff[h] = ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+                const int j = multi ? fdiv(m, g.dOHW) : 0;     // image inside the chunk
+                const int pm = m - j * ohw;
+                const int oh = fdiv(pm, g.dOW);
+                const int ow = pm - oh * g.OW;
+                roff[h] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
             }
             const int mr = sub * 32 + grp * 8 + q;
             Frag fa[TF], fbk[TK];

@@ -305,8 +305,20 @@ def conv_lds_config(geo: dict, N: int):
     return None
 
 
+def conv_wgrad_ipc(geo: dict, tier: int) -> int:
+    """Whole images per 128-row chunk of the conv WGRAD kernel (gemm3.hip g3_conv_wgrad_kernel):
+    min(128 // (OH*OW), patch capacity // (H*W*Cs)) when that is >= 2, else 1 (per-image pixel tiles)."""
+    H, W, C, OH, OW = (int(geo[k]) for k in ("H", "W", "C", "OH", "OW"))
+    cp = -(-C // 8) * 8
+    cs = cp if (cp // 8) % 2 == 1 else cp + 8
+    ohw = OH * OW
+    ipc = min(128 // ohw, CONV_PATCH_TIERS[tier] // (H * W * cs)) if ohw < 128 else 0
+    return ipc if ipc >= 2 else 1
+
+
 def conv_wgrad_config(geo: dict, F: int):
-    """(BMF, BNK, patch tier) for the LDS-halo conv WGRAD kernel (128-pixel chunks), or None."""
+    """(BMF, BNK, patch tier) for the LDS-halo conv WGRAD kernel (128-pixel chunks), or None.  Small
+    outputs take the smallest tier that packs all the images a chunk can hold (multi-image chunks)."""
     KH, KW, C, W, OH, OW, SH = (int(geo[k]) for k in ("KH", "KW", "C", "W", "OH", "OW", "SH"))
     if KH * KW <= 1 or "conv_wgrad" in _OFF:
         return None
@@ -317,6 +329,11 @@ def conv_wgrad_config(geo: dict, F: int):
     tier = next((i for i, cap in enumerate(CONV_PATCH_TIERS) if need <= cap), None)
     if tier is None:
         return None
+    if OH * OW < 128 and "conv_wgrad_multi" not in _OFF:
+        want = 128 // (OH * OW)
+        best = max(range(len(CONV_PATCH_TIERS)), key=lambda t_: (min(conv_wgrad_ipc(geo, t_), want), -t_))
+        if conv_wgrad_ipc(geo, best) >= 2:
+            tier = best
     kp = KH * KW * cp
     bmf = 16 if F <= 16 else (32 if F <= 32 else 64)
     if bmf == 64:
@@ -456,9 +473,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
         elif v >= 3000000 and mode == MODE_WGRAD:
             bmf, bnk = (v % 100000) // 1000, v % 1000
             tl = []
+            tier = (v // 100000) % 10
             for p, (r, (M, N, K)) in enumerate(items):
                 ohw = int(r["OH"]) * int(r["OW"])
-                nchunks = (K // ohw) * (-(-ohw // 128))
+                ipc = conv_wgrad_ipc(r, tier)
+                nchunks = -(-(K // ohw) // ipc) if ipc >= 2 else (K // ohw) * (-(-ohw // 128))
                 cp = -(-int(r["C"]) // 8) * 8
                 nkt = -(-(int(r["KH"]) * int(r["KW"]) * cp) // bnk)
                 nft = -(-M // bmf)

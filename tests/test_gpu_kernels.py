@@ -99,6 +99,10 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     (30, 100, 1, 1, 75, 1, 1, 1, 1, "relu"),      # narrow + LDS-staged rows (N % 8 != 0): g Dense(75)
     (30, 100, 1, 2, 37, 1, 1, 1, 1, "sigmoid"),   # staged, K = 2, multi-pass blocks with a ragged tail
     (13, 100, 1, 1, 130, 1, 1, 1, 1, "relu"),     # staged, N > 128 (several FWD passes per block)
+    # small conv outputs: the conv WGRAD kernel packs several whole images into one 128-row chunk
+    # (5x5 outputs: 3 images per chunk, a ragged last chunk; 8x8 outputs: 2 images per chunk)
+    (17, 11, 11, 64, 16, 7, 7, 1, 1, "relu"),
+    (9, 12, 12, 32, 24, 5, 5, 1, 1, "linear"),
     # wide-f WGRAD tiles (F > 64: one 128- or 256-row f tile per layer)
     (9, 1, 1, 300, 200, 1, 1, 1, 1, "relu"),
     (40, 5, 1, 96, 120, 1, 1, 1, 1, "sigmoid"),

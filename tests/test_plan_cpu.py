@@ -97,3 +97,21 @@ def test_gchain_variant_and_block_sizing():
             assert rpb % 64 == 0 and rpb >= 64
             # the block's genotype rows fit the kernel's LDS staging buffer
             assert (-(-rpb // l1) + 1) * 100 <= H.GCHAIN_GMAX
+
+
+def test_conv_wgrad_multi_image_chunks():
+    """Small conv outputs pack whole images into the 128-row chunks of the conv WGRAD kernel; the
+    tier is chosen to hold as many as a chunk can take, and large outputs keep per-image tiles."""
+    g = dict(KH=7, KW=7, C=64, H=11, W=11, OH=5, OW=5, SH=1)
+    bmf, bnk, tier = H.conv_wgrad_config(g, 16)
+    assert H.conv_wgrad_ipc(g, tier) == 3                    # 3 x 11*11*72 <= 32768 < 4 x ...
+    g = dict(KH=5, KW=5, C=32, H=12, W=12, OH=8, OW=8, SH=1)
+    assert H.conv_wgrad_ipc(g, H.conv_wgrad_config(g, 16)[2]) == 2
+    g = dict(KH=3, KW=3, C=73, H=24, W=24, OH=22, OW=22, SH=1)
+    assert H.conv_wgrad_ipc(g, H.conv_wgrad_config(g, 16)[2]) == 1
+    # the tile table covers every image exactly once
+    rows = [dict(a=0, b=0, out=0, H=11, W=11, C=64, OH=5, OW=5, F=16, KH=7, KW=7, SH=1, SW=1, M=16, N=3136,
+                 K=17 * 25, flags=0)]
+    (v, rws, tiles), = H.gemm3_plan(H.MODE_WGRAD, rows, [(16, 3136, 17 * 25)])
+    assert v >= 3000000
+    assert int(tiles[:, 3].max()) == 6 and int(tiles[:, 2].min()) == 0      # ceil(17 / 3) chunks
