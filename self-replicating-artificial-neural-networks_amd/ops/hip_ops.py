@@ -474,6 +474,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             bmf, bnk = (v % 100000) // 1000, v % 1000
             tl = []
             tier = (v // 100000) % 10
+            geo = []
             for p, (r, (M, N, K)) in enumerate(items):
                 ohw = int(r["OH"]) * int(r["OW"])
                 ipc = conv_wgrad_ipc(r, tier)
@@ -481,7 +482,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 cp = -(-int(r["C"]) // 8) * 8
                 nkt = -(-(int(r["KH"]) * int(r["KW"]) * cp) // bnk)
                 nft = -(-M // bmf)
-                per = min(64, max(8, -(-nchunks // 64)))
+                geo.append((nchunks, nkt, nft, min(64, max(8, -(-nchunks // 64)))))
+            # (chunks per block 8..64: unlike the GEMM WGRAD, more and shorter blocks measured slower --
+            # every block restages its patches and the cross-chunk prefetch needs a long chunk range)
+            for p, (r, (M, N, K)) in enumerate(items):
+                nchunks, nkt, nft, per = geo[p]
                 for c0 in range(0, nchunks, per):
                     c1 = min(nchunks, c0 + per)
                     ff, kk = np.meshgrid(np.arange(nft), np.arange(nkt), indexing="ij")
@@ -495,6 +500,12 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             if mode == MODE_WGRAD:
                 tg = [wgrad_target(M, N) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
+                # a launch of few blocks leaves most of the 256 CUs idle (measured: 57 blocks for two
+                # [70 x 98] Dense WGRADs over 75000 rows ran at 0.2 TB/s): split the reductions finer
+                # until the launch fills the GPU (the extra fp32 atomics are per-block output tiles)
+                while len(tiles) < WGRAD_MIN_BLOCKS and max(tg) > 16 and "wgrad_minblocks" not in _OFF:
+                    tg = [max(16, t_ // 2) for t_ in tg]
+                    tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
@@ -571,6 +582,7 @@ def wgrad_target(M: int, N: int) -> int:
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # per grouped launch
 _WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
