@@ -310,13 +310,16 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
     for (int nt = 0; nt < NT; ++nt) bsum[nt] = 0.f;
 
     bf16_t* slot = img[wave];
-    const int b0 = ic * CP_WGRAD_IMGS;
+    // images per block: d.flags when set (a multiple of 4: hip_ops.convpool_wgrad_imgs lowers it for
+    // launches of few blocks), else CP_WGRAD_IMGS
+    const int ipb = d.flags > 0 ? (int)d.flags : CP_WGRAD_IMGS;
+    const int b0 = ic * ipb;
     CpStager st;
     st.start(d, b0 + wave, lane);
-    for (int it = 0; it < CP_WGRAD_IMGS / 4; ++it) {
+    for (int it = 0; it < ipb / 4; ++it) {
         const int b = b0 + it * 4 + wave;
         __syncthreads();
-        st.stage(d, slot, b, it + 1 < CP_WGRAD_IMGS / 4 ? b + 4 : Bn, lane);
+        st.stage(d, slot, b, it + 1 < ipb / 4 ? b + 4 : Bn, lane);
         __syncthreads();
         if (b >= Bn) continue;
         for (int pk = 0; pk < npos; pk += 32) {

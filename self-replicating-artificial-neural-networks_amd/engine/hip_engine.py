@@ -746,8 +746,11 @@ class HipPopulationEngine(PopulationEngine):
                 by_kt.setdefault(r.pop("_kt"), []).append(r)
             for kt in sorted(by_kt):
                 rws = by_kt[kt]
+                imgs = H.convpool_wgrad_imgs([(r["B"], r["F"]) for r in rws]) if backward else 0
+                for r in rws:
+                    r["flags"] = imgs
                 add_chunked("convpool", (1 if backward else 0, kt), rws, H.CONVPOOL_DTYPE,
-                            [H.convpool_chunks(r["B"], r["F"], backward) for r in rws], 1)
+                            [H.convpool_chunks(r["B"], r["F"], backward, imgs) for r in rws], 1)
         def gchain_row(o, last):
             """Descriptor of the fused genotype chain ending at node ``last`` of organism ``o``."""
             lay_ = self.layouts[o]

@@ -158,10 +158,21 @@ def gchain_rpb(rows: int, nprob: int, mode: int, l1: int = 1, l0: int = 0) -> in
     return rpb
 
 
-def convpool_chunks(batch: int, filters: int, backward: bool) -> int:
-    """Blocks of one fused conv+pool problem: image chunks x groups of 64 filters."""
-    per = CONVPOOL_WGRAD_IMGS if backward else CONVPOOL_FWD_IMGS
+def convpool_chunks(batch: int, filters: int, backward: bool, imgs: int = 0) -> int:
+    """Blocks of one fused conv+pool problem: image chunks x groups of 64 filters (``imgs``: images
+    per WGRAD block, default CONVPOOL_WGRAD_IMGS)."""
+    per = (imgs or CONVPOOL_WGRAD_IMGS) if backward else CONVPOOL_FWD_IMGS
     return -(-int(batch) // per) * -(-int(filters) // 64)
+
+
+def convpool_wgrad_imgs(problems) -> int:
+    """Images per block of a grouped fused conv+pool WGRAD launch over (batch, filters) problems:
+    32, halved (down to 8) while the launch has fewer than WGRAD_MIN_BLOCKS blocks."""
+    imgs = CONVPOOL_WGRAD_IMGS
+    while imgs > 8 and "wgrad_minblocks" not in _OFF and \
+            sum(convpool_chunks(b, f, True, imgs) for b, f in problems) < WGRAD_MIN_BLOCKS:
+        imgs //= 2
+    return imgs
 
 
 def red_chunks(rows: int, channels: int) -> int:
