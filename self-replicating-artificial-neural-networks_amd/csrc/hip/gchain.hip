@@ -107,11 +107,9 @@ __device__ __forceinline__ void gc_tr_read(GcFrag& f, const __attribute__((addre
         (__attribute__((address_space(3))) gc_s16x4_t*)(img + row * ld + col));
     const gc_s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) gc_s16x4_t*)(img + (row + 4) * ld + col));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        f.h[e] = (bf16_t)lo[e];
-        f.h[4 + e] = (bf16_t)hi[e];
-    }
+    // vector shuffle + bit cast (an element-wise copy leaves v_bfi no-ops beside the MFMAs)
+    typedef __attribute__((ext_vector_type(8))) short gc_s16x8_t;
+    f.v = __builtin_bit_cast(gc_bf16x8_t, (gc_s16x8_t)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // Global-memory accesses through address space 1: descriptor pointers are generic, and flat

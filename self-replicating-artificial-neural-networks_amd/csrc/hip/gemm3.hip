@@ -136,6 +136,17 @@ __device__ __forceinline__ uint4 mul_act_grad(uint4 dy, uint4 yv, int act) {
     return out.u;
 }
 
+// Two transposing LDS reads (rows r and r + 4 of a 16-column quad) -> one MFMA fragment.  A vector
+// shuffle + bit cast: no per-element moves (an element-wise copy through bf16_t left v_bfi no-ops in
+// the MFMA loops).
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+__device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_p, const bf16_t* hi_p) {
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(lo_p));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(hi_p));
+    const s16x8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // ---- im2col chunk (FWD A operand, WGRAD B operand) -------------------------------------------
 // Per-lane decomposition of the reduction chunk starting at k = (kh, kw, c).
 struct KChunk {
@@ -536,8 +547,11 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
     // two register sets: the loads of 64-row step i+1 are issued one full step before step i+1 is
     // staged, so every global load has two MFMA steps (not one) to land -- the loop is load-latency
     // bound for the streaming (many rows, small F x N) problems
-    Frag ra0[APASS], rb0[BPASS], ra1[APASS], rb1[BPASS];
-    auto load = [&](int kt, Frag (&ra)[APASS], Frag (&rbv)[BPASS]) {
+    // dY and Y are loaded raw and dZ = dY * act'(Y) is formed when the step is staged: forming it
+    // at load time made the wave wait for the loads it had just issued (s_waitcnt vmcnt(0) before the
+    // MFMAs of the current step), which defeated the register double buffer
+    Frag ra0[APASS], rb0[BPASS], ra1[APASS], rb1[BPASS], ry0[APASS], ry1[APASS];
+    auto load = [&](int kt, Frag (&ra)[APASS], Frag (&ry)[APASS], Frag (&rbv)[BPASS]) {
         const int m0 = kt * 32;
 #pragma unroll
         for (int p = 0; p < APASS; ++p) {
@@ -545,10 +559,8 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
             const int m = m0 + r;
             const bool ok = a_act && r < BKM && a_nv > 0 && m < mlim;
             const int off = ok ? m * g.F + f0 + a_f : -1;
-            uint4 v = bl16(rZ, off);
-            if (g.act != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), g.act);
-            if (a_nv < 8) v = splice(v, make_uint4(0, 0, 0, 0), a_nv);
-            ra[p].u = v;
+            ra[p].u = bl16(rZ, off);
+            if (g.act != ACT_LINEAR) ry[p].u = bl16(rY, off);
         }
 #pragma unroll
         for (int p = 0; p < BPASS; ++p) {
@@ -570,11 +582,15 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
             }
         }
     };
-    auto stash = [&](const Frag (&ra)[APASS], const Frag (&rbv)[BPASS]) {
+    auto stash = [&](Frag (&ra)[APASS], const Frag (&ry)[APASS], const Frag (&rbv)[BPASS]) {
 #pragma unroll
         for (int p = 0; p < APASS; ++p) {
+            uint4 v = ra[p].u;
+            if (g.act != ACT_LINEAR) v = mul_act_grad(v, ry[p].u, g.act);
+            if (a_nv < 8) v = splice(v, make_uint4(0, 0, 0, 0), a_nv);
+            ra[p].u = v;                                 // (bias_acc reads dZ)
             const int r = a_r + p * AROWS;
-            if (a_act && r < BKM) *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = ra[p].u;
+            if (a_act && r < BKM) *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = v;
         }
 #pragma unroll
         for (int p = 0; p < BPASS; ++p)
@@ -597,32 +613,22 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             const int mr = sub * 32 + grp * 8 + q;
-            Frag fa[TF], fbk[TK];
+            bf16x8_t fa[TF], fbk[TK];
 #pragma unroll
             for (int i = 0; i < TF; ++i) {
                 const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
-                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&As[mr * LDA + col]));
-                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&As[(mr + 4) * LDA + col]));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { fa[i].h[e] = (bf16_t)lo[e]; fa[i].h[4 + e] = (bf16_t)hi[e]; }
+                fa[i] = tr_frag(&As[mr * LDA + col], &As[(mr + 4) * LDA + col]);
             }
 #pragma unroll
             for (int j = 0; j < TK; ++j) {
                 const int col = wk * (BNK / WC) + j * 16 + 4 * pp;
-                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[mr * LDB + col]));
-                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(mr + 4) * LDB + col]));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { fbk[j].h[e] = (bf16_t)lo[e]; fbk[j].h[4 + e] = (bf16_t)hi[e]; }
+                fbk[j] = tr_frag(&Bs[mr * LDB + col], &Bs[(mr + 4) * LDB + col]);
             }
 #pragma unroll
             for (int i = 0; i < TF; ++i)
 #pragma unroll
                 for (int j = 0; j < TK; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fbk[j].v, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbk[j], acc[i][j], 0, 0, 0);
         }
     };
     auto bias_acc = [&](const Frag (&ra)[APASS]) {
@@ -637,38 +643,38 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
     // kt counts 32-row units; one step consumes two of them (64 rows); steps rotate over WG_NSETS
     // register sets, so the loads of a step are issued WG_NSETS steps before it is staged
 #if WG_NSETS == 2
-    if (kt0 < kt1) load(kt0, ra0, rb0);
-    if (kt0 + 2 < kt1) load(kt0 + 2, ra1, rb1);
+    if (kt0 < kt1) load(kt0, ra0, ry0, rb0);
+    if (kt0 + 2 < kt1) load(kt0 + 2, ra1, ry1, rb1);
     for (int kt = kt0; kt < kt1; kt += 4) {
         __syncthreads();
-        stash(ra0, rb0);
+        stash(ra0, ry0, rb0);
         bias_acc(ra0);
         __syncthreads();
-        if (kt + 4 < kt1) load(kt + 4, ra0, rb0);
+        if (kt + 4 < kt1) load(kt + 4, ra0, ry0, rb0);
         compute();
         if (kt + 2 >= kt1) break;
         __syncthreads();
-        stash(ra1, rb1);
+        stash(ra1, ry1, rb1);
         bias_acc(ra1);
         __syncthreads();
-        if (kt + 6 < kt1) load(kt + 6, ra1, rb1);
+        if (kt + 6 < kt1) load(kt + 6, ra1, ry1, rb1);
         compute();
     }
 #else
-    Frag rax[WG_NSETS][APASS], rbx[WG_NSETS][BPASS];
+    Frag rax[WG_NSETS][APASS], ryx[WG_NSETS][APASS], rbx[WG_NSETS][BPASS];
 #pragma unroll
     for (int q_ = 0; q_ < WG_NSETS; ++q_)
-        if (kt0 + 2 * q_ < kt1) load(kt0 + 2 * q_, rax[q_], rbx[q_]);
+        if (kt0 + 2 * q_ < kt1) load(kt0 + 2 * q_, rax[q_], ryx[q_], rbx[q_]);
     for (int kt = kt0; kt < kt1; kt += 2 * WG_NSETS) {
 #pragma unroll
         for (int q_ = 0; q_ < WG_NSETS; ++q_) {
             const int kc = kt + 2 * q_;
             if (kc >= kt1) break;
             __syncthreads();
-            stash(rax[q_], rbx[q_]);
+            stash(rax[q_], ryx[q_], rbx[q_]);
             bias_acc(rax[q_]);
             __syncthreads();
-            if (kc + 2 * WG_NSETS < kt1) load(kc + 2 * WG_NSETS, rax[q_], rbx[q_]);
+            if (kc + 2 * WG_NSETS < kt1) load(kc + 2 * WG_NSETS, rax[q_], ryx[q_], rbx[q_]);
             compute();
         }
     }
@@ -880,6 +886,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     // patch + one 16-B dump slot for the staging writes of pieces past the chunk's patch
     __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH + 8];
     __shared__ __attribute__((aligned(16))) bf16_t As[TM * LDA];
+    __shared__ int rtab[TM];              // per chunk row: patch element offset of its receptive field
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
@@ -956,7 +963,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     // behind compute (one LDS copy of each operand; two barriers per chunk).
     constexpr int PLD = PATCH / 2048;               // 16-B patch pieces per thread (max)
     constexpr int ALD = (TM * ACH + 255) / 256;     // 16-B dZ pieces per thread
-    uint4 pre[PLD], apre[ALD];
+    uint4 pre[PLD], apre[ALD], ypre[ALD];
     int cur_npix = 0;
     auto fetch = [&](int ch) {
         int b, m0, m_last;
@@ -979,25 +986,17 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             const int c = u * 8 - p * Cp;
             pre[k] = bl16(rX, p < npix ? gbase + p * g.C + c : -1);
         }
-        if (g.C & 7) {                                 // zero the pad channels (not in the K range)
-#pragma unroll
-            for (int k = 0; k < PLD; ++k) {
-                const int u = t + k * 256;
-                const int p = fdiv(u * 8, dCp);
-                const int c = u * 8 - p * Cp;
-                pre[k] = splice(pre[k], zero, g.C - c);
-            }
-        }
+        // C % 8 != 0: the pad channels of a pixel hold the next pixel's first channels.  They are left
+        // as they are: a pad channel only feeds the accumulator columns (tap, c >= C), which the flush
+        // never stores (zeroing them per piece kept ~60 loop-invariant lane masks live: SGPR spills)
 #pragma unroll
         for (int k = 0; k < ALD; ++k) {
             const int r = a_r0 + k * AROWS;
             const int m = m0 + r;
             const bool ok = r < TM && a_nv > 0 && m <= m_last;
             const int off = ok ? (b * ohw + m) * g.F + f0 + a_f : -1;
-            uint4 v = bl16(rZ, off);
-            if (g.act != ACT_LINEAR) v = mul_act_grad<false>(v, bl16(rY, off), g.act);
-            if (a_nv < 8) v = splice(v, zero, a_nv);
-            apre[k] = v;
+            apre[k] = bl16(rZ, off);                  // raw: act' is applied when staged (as in
+            if (g.act != ACT_LINEAR) ypre[k] = bl16(rY, off);   // g3_wgrad_kernel)
         }
     };
 
@@ -1015,14 +1014,29 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             const int c = u * 8 - p * Cp;
             *reinterpret_cast<uint4*>(&patch[p < npix ? p * Cs + c : PATCH]) = pre[k];
         }
+        if (t < TM) {
+            // row offsets, once per chunk (the MFMA loop reads them instead of redoing the
+            // pixel -> (image, oh, ow) divisions per lane, sub-step and row quad); rows past the chunk
+            // end read a valid pixel (their dZ rows are zero)
+            int m = m0 + t;
+            if (m > m_last) m = m0;
+            const int j = multi ? fdiv(m, g.dOHW) : 0;     // image inside the chunk
+            const int pm = m - j * ohw;
+            const int oh = fdiv(pm, g.dOW);
+            const int ow = pm - oh * g.OW;
+            rtab[t] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+        }
 #pragma unroll
         for (int k = 0; k < ALD; ++k) {
             const int r = a_r0 + k * AROWS;
             if (r < TM) {
-                *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = apre[k];
+                uint4 v = apre[k];
+                if (g.act != ACT_LINEAR) v = mul_act_grad(v, ypre[k], g.act);
+                if (a_nv < 8) v = splice(v, zero, a_nv);
+                *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = v;
                 if (do_bias) {
                     Frag fv;
-                    fv.u = apre[k];
+                    fv.u = v;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) bsum[j] += bf2f(fv.h[j]);
                 }
@@ -1032,45 +1046,23 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         if (ch + 1 < td.w) fetch(ch + 1);
 #pragma unroll
         for (int sub = 0; sub < TM / 32; ++sub) {
-            // rows of this lane's two tr-read quads; rows past the chunk end read a valid pixel
-            // (their dZ rows are zero)
-            int roff[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                int m = m0 + sub * 32 + grp * 8 + 4 * h + q;
-                if (m > m_last) m = m0;
-                const int j = multi ? fdiv(m, g.dOHW) : 0;     // image inside the chunk
-                const int pm = m - j * ohw;
-                const int oh = fdiv(pm, g.dOW);
-                const int ow = pm - oh * g.OW;
-                roff[h] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
-            }
+            // rows of this lane's two tr-read quads
             const int mr = sub * 32 + grp * 8 + q;
-            Frag fa[TF], fbk[TK];
+            const bf16_t* p0 = patch + rtab[mr];
+            const bf16_t* p1 = patch + rtab[mr + 4];
+            bf16x8_t fa[TF], fbk[TK];
 #pragma unroll
             for (int i = 0; i < TF; ++i) {
                 const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
-                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&As[mr * LDA + col]));
-                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&As[(mr + 4) * LDA + col]));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { fa[i].h[e] = (bf16_t)lo[e]; fa[i].h[4 + e] = (bf16_t)hi[e]; }
+                fa[i] = tr_frag(&As[mr * LDA + col], &As[(mr + 4) * LDA + col]);
             }
 #pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&patch[roff[0] + coff[j]]));
-                s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&patch[roff[1] + coff[j]]));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { fbk[j].h[e] = (bf16_t)lo[e]; fbk[j].h[4 + e] = (bf16_t)hi[e]; }
-            }
+            for (int j = 0; j < TK; ++j) fbk[j] = tr_frag(p0 + coff[j], p1 + coff[j]);
 #pragma unroll
             for (int i = 0; i < TF; ++i)
 #pragma unroll
                 for (int j = 0; j < TK; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fbk[j].v, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbk[j], acc[i][j], 0, 0, 0);
         }
     }
 
@@ -1733,12 +1725,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
             for (int j = 0; j < NTW; ++j) {
                 const int colb = wc * (BN / 2) + j * 16 + 4 * pp;
-                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(buf * BK + grp * 8 + q) * LDBT + colb]));
-                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (__attribute__((address_space(3))) s16x4_t*)(&Bs[(buf * BK + grp * 8 + 4 + q) * LDBT + colb]));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { fb[j].h[e] = (bf16_t)lo[e]; fb[j].h[4 + e] = (bf16_t)hi[e]; }
+                fb[j].v = tr_frag(&Bs[(buf * BK + grp * 8 + q) * LDBT + colb], &Bs[(buf * BK + grp * 8 + 4 + q) * LDBT + colb]);
             }
         } else {
 #pragma unroll
