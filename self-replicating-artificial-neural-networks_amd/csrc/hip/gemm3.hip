@@ -61,6 +61,11 @@ __device__ __forceinline__ uint4 bl16(rsrc_t r, int elem) {       // 8 bf16 at e
     f.q = __builtin_amdgcn_raw_buffer_load_b128(r, elem < 0 ? OOB : elem * 2, 0, 0);
     return f.u;
 }
+__device__ __forceinline__ uint4 bl16b(rsrc_t r, int byteoff) {   // 8 bf16 at a byte offset (OOB: zeros)
+    Frag f;
+    f.q = __builtin_amdgcn_raw_buffer_load_b128(r, byteoff, 0, 0);
+    return f.u;
+}
 __device__ __forceinline__ bf16_t bl1(rsrc_t r, int elem) {
     return __builtin_amdgcn_raw_buffer_load_b16(r, elem * 2, 0, 0);
 }
@@ -550,17 +555,41 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
     // dY and Y are loaded raw and dZ = dY * act'(Y) is formed when the step is staged: forming it
     // at load time made the wave wait for the loads it had just issued (s_waitcnt vmcnt(0) before the
     // MFMAs of the current step), which defeated the register double buffer
+    // Row-affine operands: a load's byte offset is a per-thread constant plus the step's row base
+    // m0 * row bytes (one scalar), and rows >= mlim (the next m split) are masked by one compare against
+    // a per-thread row key (2^30 for threads without a chunk).  dZ / Y are [K][F] row-major always; X is
+    // when the layer is 1x1 stride 1 (row m of the im2col is input row m).  For those, lanes past a
+    // row's last column (the next row's data) only feed accumulator columns that are never stored.
+    int aoff[APASS], akey[APASS], boff[BPASS], bkey[BPASS];
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) {
+        const int r = a_r + p * AROWS;
+        const bool v = a_act && r < BKM && a_nv > 0;
+        aoff[p] = (r * g.F + f0 + a_f) * 2;
+        akey[p] = v ? r : (1 << 30);
+    }
+#pragma unroll
+    for (int p = 0; p < BPASS; ++p) {
+        const int r = b_r + p * BROWS;
+        boff[p] = (r * g.C + kk) * 2;
+        bkey[p] = (r < BKM && kk < g.N) ? r : (1 << 30);
+    }
     Frag ra0[APASS], rb0[BPASS], ra1[APASS], rb1[BPASS], ry0[APASS], ry1[APASS];
     auto load = [&](int kt, Frag (&ra)[APASS], Frag (&ry)[APASS], Frag (&rbv)[BPASS]) {
         const int m0 = kt * 32;
+        const int lim = mlim - m0;                   // rows of this step inside the split
+        const int sa = m0 * g.F * 2;
 #pragma unroll
         for (int p = 0; p < APASS; ++p) {
-            const int r = a_r + p * AROWS;
-            const int m = m0 + r;
-            const bool ok = a_act && r < BKM && a_nv > 0 && m < mlim;
-            const int off = ok ? m * g.F + f0 + a_f : -1;
-            ra[p].u = bl16(rZ, off);
-            if (g.act != ACT_LINEAR) ry[p].u = bl16(rY, off);
+            const int off = akey[p] < lim ? aoff[p] + sa : OOB;
+            ra[p].u = bl16b(rZ, off);
+            if (g.act != ACT_LINEAR) ry[p].u = bl16b(rY, off);
+        }
+        if (pix1) {
+            const int sb = m0 * g.C * 2;
+#pragma unroll
+            for (int p = 0; p < BPASS; ++p) rbv[p].u = bl16b(rX, bkey[p] < lim ? boff[p] + sb : OOB);
+            return;
         }
 #pragma unroll
         for (int p = 0; p < BPASS; ++p) {
@@ -1652,18 +1681,22 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     constexpr int NCH = BN / 8, BKP = 256 / NCH, BTP = (BK + BKP - 1) / BKP;
     const int bkr = t / NCH, bnc = (t % NCH) * 8;
     const bool bt_act = t < NCH * BKP;
-    uint4 ra[2], rb[BT ? BTP : BPT];
+    // DGRAD: dY and Y load raw and dZ = dY * act'(Y) is formed in sstore(), after the MFMAs of the
+    // current step (forming it here made the step wait for the loads of the next one).  Measured
+    // slower in g3_direct_kernel, whose fragments stay in registers: there the extra Y registers of
+    // both pipeline sets cost a wave per SIMD (profiles/r2e/kb_dgrad_compare.txt)
+    uint4 ra[2], ry[2], rb[BT ? BTP : BPT];
+    int arun = 8;
     auto gload = [&](int kt) {
         const int k = kt * BK + lk;
         const int run = min(8, K - k);
+        arun = run;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int m = m0 + lr + 64 * i;
             const int off = (m < M && run > 0) ? m * lda + k : -1;
-            uint4 v = bl16(rA, off);
-            if (gact != ACT_LINEAR) v = mul_act_grad(v, bl16(rY, off), gact);
-            if (run < 8) v = splice(v, zero, run);
-            ra[i] = v;
+            ra[i] = bl16(rA, off);
+            if (gact != ACT_LINEAR) ry[i] = bl16(rY, off);
         }
         if (BT) {
 #pragma unroll
@@ -1688,8 +1721,12 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     };
     auto sstore = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lk]) = ra[i];
+        for (int i = 0; i < 2; ++i) {
+            uint4 v = ra[i];
+            if (gact != ACT_LINEAR) v = mul_act_grad(v, ry[i], gact);
+            if (arun < 8) v = splice(v, zero, arun);
+            *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lk]) = v;
+        }
         if (BT) {
 #pragma unroll
             for (int i = 0; i < BTP; ++i)
