@@ -40,6 +40,14 @@ def test_wgrad_variants_default_to_64_row_tiles():
     assert H.gemm3_block(H.MODE_WGRAD, 160628) == (160, 128)
 
 
+def test_wgrad_96_row_tile_for_units_just_above_64():
+    # F in (64, 96]: one 96-row f tile (a second 64-row tile would be mostly empty)
+    assert H.gemm3_variant(H.MODE_WGRAD, 73, 64, 432000, {}) == 96064
+    assert H.gemm3_block(H.MODE_WGRAD, 96064) == (96, 64)
+    assert H.gemm3_variant(H.MODE_WGRAD, 64, 64, 432000, {}) == 64064
+    assert H.gemm3_variant(H.MODE_WGRAD, 97, 64, 432000, {}) == 64064
+
+
 @pytest.mark.parametrize("name,fused", [("convpool_bench_a", True), ("convpool_k9_f80", True),
                                         ("conv_pool_dense", True), ("odd_channels_bn", False),
                                         ("conv1d_rank4_and_strided_pool", False), ("bn_first_and_pool3", False)])
