@@ -1959,7 +1959,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
-        W3(128, 128) W3(160, 128) W3(128, 64) W3(160, 64)
+        W3(128, 128) W3(160, 128) W3(128, 64) W3(160, 64) W3(96, 64)
 #define W8(BMF_, BNK_) \
     if (v == BMF_ * 1000 + BNK_ + 500) { \
         const dim3 b8(512); \

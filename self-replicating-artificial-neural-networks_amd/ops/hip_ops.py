@@ -258,6 +258,10 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
             return bmf * 1000 + (128 if N > 64 else 64) + (1000000 if im2col_gen else 0)
         if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
             return 64 * 1000 + 16 + (1000000 if im2col_gen else 0)
+        if 64 < M <= 96 and _WGRAD_96:
+            # Dense units just above 64 (the generator's N(64, 8) / N(64, 15) draws): one 96-row f tile
+            # instead of a full 64-row tile plus a mostly empty second one (X read once, 25 % fewer MFMAs)
+            return 96 * 1000 + 64 + (1000000 if im2col_gen else 0)
 
         if bmf == 16:
             bnk = 256 if N > 128 else (128 if N > 64 else 64)
@@ -594,6 +598,7 @@ def wgrad_target(M: int, N: int) -> int:
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # per grouped launch
+_WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "1") != "0"  # 96-row f tile for 64 < F <= 96 (A/B switch)
 _WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
