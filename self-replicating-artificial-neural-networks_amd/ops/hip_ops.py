@@ -598,7 +598,9 @@ def wgrad_target(M: int, N: int) -> int:
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # per grouped launch
-_WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "1") != "0"  # 96-row f tile for 64 < F <= 96 (A/B switch)
+# 96-row f tile for 64 < F <= 96: opt-in, measured slower (population B step 19.9 -> 29.1 ms: the
+# 96-row blocks drop to 2 waves per SIMD and stage 4 A passes per step; profiles/r2e/ab_wgrad96.txt)
+_WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "0") == "1"
 _WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 

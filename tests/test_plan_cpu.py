@@ -40,8 +40,10 @@ def test_wgrad_variants_default_to_64_row_tiles():
     assert H.gemm3_block(H.MODE_WGRAD, 160628) == (160, 128)
 
 
-def test_wgrad_96_row_tile_for_units_just_above_64():
-    # F in (64, 96]: one 96-row f tile (a second 64-row tile would be mostly empty)
+def test_wgrad_96_row_tile_is_opt_in(monkeypatch):
+    # F in (64, 96]: 64-row tiles by default; the 96-row tile (measured slower) only behind the switch
+    assert H.gemm3_variant(H.MODE_WGRAD, 73, 64, 432000, {}) == 64064
+    monkeypatch.setattr(H, "_WGRAD_96", True)
     assert H.gemm3_variant(H.MODE_WGRAD, 73, 64, 432000, {}) == 96064
     assert H.gemm3_block(H.MODE_WGRAD, 96064) == (96, 64)
     assert H.gemm3_variant(H.MODE_WGRAD, 64, 64, 432000, {}) == 64064
