@@ -608,7 +608,8 @@ _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,
                bn: int = BN, swizzle: bool = False) -> np.ndarray:
     """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16).
-    target_ksteps: int, or one value per problem (WGRAD m-split granularity)."""
+    target_ksteps: int, or one value per problem (WGRAD m-split granularity).  Vectorised over the k
+    splits of a problem (a WGRAD over 432k rows has hundreds): plans are rebuilt every generation."""
     rows = []
     for p, (M, N, K) in enumerate(dims):
         tm, tn = -(-M // bm), -(-N // bn)
@@ -620,19 +621,22 @@ def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int
         if mode == MODE_WGRAD:
             nsplit = wgrad_splits(K, tgt, min(min_ksteps, tgt))
         per = -(-kt // nsplit)
+        k0 = np.arange(nsplit, dtype=np.int64) * per
+        k1 = np.minimum(kt, k0 + per)
+        packed = (k0 | (k1 << 16))[k0 < k1]
         # k-split outermost, then n, then m: consecutive blocks share the weight (B) panel
-        for s in range(nsplit):
-            k0, k1 = s * per, min(kt, (s + 1) * per)
-            if k0 >= k1:
-                continue
-            packed = k0 | (k1 << 16)
-            mm, nn = np.meshgrid(np.arange(tm), np.arange(tn), indexing="xy")
-            blk = np.stack([np.full(tm * tn, p), mm.ravel(), nn.ravel(), np.full(tm * tn, packed)], 1)
-            if swizzle:
-                # m fastest: the tm tiles of one n column share its B panel (WGRAD: the X columns,
-                # DGRAD: the weight columns) -> keep them on one XCD
-                blk = xcd_swizzle(blk, tm)
-            rows.append(blk)
+        T = tm * tn
+        idx = np.arange(T)
+        blk = np.empty((len(packed), T, 4), np.int64)
+        blk[:, :, 0] = p
+        blk[:, :, 1] = idx % tm
+        blk[:, :, 2] = idx // tm
+        blk[:, :, 3] = packed[:, None]
+        if swizzle:
+            # m fastest: the tm tiles of one n column share its B panel (WGRAD: the X columns,
+            # DGRAD: the weight columns) -> keep them on one XCD
+            blk = blk[:, xcd_order(T, tm)]
+        rows.append(blk.reshape(-1, 4))
     if not rows:
         return np.zeros((0, 4), np.int32)
     return np.concatenate(rows).astype(np.int32)
@@ -649,17 +653,21 @@ def xcd_swizzle(tiles: np.ndarray, group: int) -> np.ndarray:
     hit that XCD's L2 instead of going to the Infinity Cache / HBM once per XCD.  Tiles are independent
     (disjoint outputs or atomics), so the order is a pure performance choice; the tail that does not
     fill 8 whole groups keeps its natural order."""
-    n = len(tiles)
+    return tiles[xcd_order(len(tiles), group)]
+
+
+def xcd_order(n: int, group: int) -> np.ndarray:
+    """Gather order of xcd_swizzle: swizzled = tiles[xcd_order(len(tiles), group)]."""
     g = int(group)
+    order = np.arange(n)
     if not XCD_SWIZZLE or g <= 1 or n < XCDS * g:
-        return tiles
+        return order
     full = (n // (XCDS * g)) * XCDS * g
     i = np.arange(full)
     k, j = i // g, i % g
     pos = ((k // XCDS) * g + j) * XCDS + (k % XCDS)
-    out = tiles.copy()
-    out[pos] = tiles[:full]
-    return out
+    order[pos] = i
+    return order
 
 
 def chunk_tiles(counts, chunk: int) -> np.ndarray:
