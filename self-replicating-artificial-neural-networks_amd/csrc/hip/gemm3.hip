@@ -786,13 +786,33 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     const uint4 zero = make_uint4(0, 0, 0, 0);
 
     // ---- stage the patch: input rows [oh_a*SH, oh_a*SH + rows_in) of image b ----------------------
-    const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * g.H * g.W * g.C * 2);
-    const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
-    for (int p = t; p < npix; p += 256) {
-        for (int c = 0; c < Cp; c += 8) {
-            uint4 v = bl16(rA, gbase + p * g.C + c);
-            if (c + 8 > g.C) v = splice(v, zero, g.C - c);
-            *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
+    const bool vpad = (g.flags & GF_VPAD) != 0;
+    if (!vpad) {
+        const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * g.H * g.W * g.C * 2);
+        const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
+        for (int p = t; p < npix; p += 256) {
+            for (int c = 0; c < Cp; c += 8) {
+                uint4 v = bl16(rA, gbase + p * g.C + c);
+                if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+                *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
+            }
+        }
+    } else {
+        // DGRAD of a stride-1 conv: the patch holds rows of dZ [B][Hr][Wr][C] zero-padded by (KH-1, KW-1)
+        // (H, W are the padded extents); padding pixels are written as zeros, never loaded
+        const int Hr = g.H - 2 * (g.KH - 1), Wr = g.W - 2 * (g.KW - 1);
+        const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * Hr * Wr * g.C * 2);
+        for (int p = t; p < npix; p += 256) {
+            const int lr = fdiv(p, g.dW);
+            const int rr = oh_a + lr - (g.KH - 1);
+            const int rc = p - lr * g.W - (g.KW - 1);
+            const bool in = rr >= 0 && rr < Hr && rc >= 0 && rc < Wr;
+            const int src = ((b * Hr + rr) * Wr + rc) * g.C;
+            for (int c = 0; c < Cp; c += 8) {
+                uint4 v = in ? bl16(rA, src + c) : zero;
+                if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+                *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
+            }
         }
     }
 
@@ -818,7 +838,7 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
         const int tap = fdiv(e, dCp);
         const int c = e - tap * Cp;
         if (bn >= BN || tap >= taps || c >= g.C) return zero;
-        uint4 v = bl16(rB, brow + tap * g.C + c);
+        uint4 v = bl16(rB, brow + (vpad ? taps - 1 - tap : tap) * g.C + c);   // VPAD: flipped kernel
         if (c + 8 > g.C) v = splice(v, zero, g.C - c);
         return v;
     };
@@ -1971,7 +1991,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
     }
-    if (mode == MODE_FWD && variant >= 2000 && variant < 3000) {
+    if ((mode == MODE_FWD || mode == MODE_DGRAD) && variant >= 2000 && variant < 3000) {   // DGRAD: GF_VPAD rows
         const int v = variant - 2000;
 #define C3T(NT_, RT_, TIER_, PATCH_)                                                                  \
     if (v == 100 * TIER_ + NT_ + 10 * RT_) {                                                          \

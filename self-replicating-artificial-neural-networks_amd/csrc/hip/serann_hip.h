@@ -30,6 +30,9 @@ enum GemmFlags : int64_t {
                           // the splits and applies bias + activation (no atomics, no zeroing)
     GF_BNSTAT = 128,      // FWD narrow kernel: also accumulate the consuming BatchNorm's phase-0 statistics
                           // into aux (shifted sums, aux[c] and aux[N + c])
+    GF_VPAD = 256,        // FWD halo conv kernel: the input is dZ of a stride-1 conv, virtually zero-padded by
+                          // (KH-1, KW-1) on every side (H, W are the padded extents) and the weights are the
+                          // transposed Wt[C][KH][KW][F] read with flipped taps: a DGRAD computed as a FWD conv
     GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
                           // into a zeroed output, the bias added by the split that starts at k = 0
 };

@@ -43,6 +43,7 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
                       + [("lb", np.float64)])
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 32, 64, 128
+GF_VPAD = 256
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -320,6 +321,23 @@ def conv_lds_config(geo: dict, N: int):
     return None
 
 
+def dgrad_as_fwd_conv(r: dict):
+    """DGRAD row of a stride-1 KHxKW > 1 convolution without an activation on its output -> the
+    equivalent FWD-halo row (GF_VPAD): a valid conv of dZ zero-padded by (KH-1, KW-1) with the flipped,
+    transposed weights Wt[C][KH][KW][F] (the row's ``b``).  None when the layer does not qualify.
+    Opt-in (SERANN_DGRAD_HALO=1): measured slower than the register-fragment DGRAD on population B
+    (conv DGRAD 2.66 -> 3.38 ms per step, step 20.07 -> 20.63 ms; profiles/r2e/ab_dgrad_halo.txt) --
+    the halo tiling was tuned for FWD shapes (few input channels, many filters), DGRAD has the reverse."""
+    KH, KW, SH, SW = (int(r.get(k, 1)) for k in ("KH", "KW", "SH", "SW"))
+    if not _DGRAD_HALO or KH * KW <= 1 or SH != 1 or SW != 1 or int(r.get("act", 0)) != 0:
+        return None
+    OH, OW, F, C = int(r["OH"]), int(r["OW"]), int(r["F"]), int(r["C"])
+    t = dict(r)
+    t.update(H=OH + 2 * (KH - 1), W=OW + 2 * (KW - 1), C=F, OH=int(r["H"]), OW=int(r["W"]), F=C, bias=0, act=0,
+             aux=0, flags=(int(r.get("flags", 0)) & GF_ACCUM) | GF_VPAD)
+    return t
+
+
 def conv_wgrad_ipc(geo: dict, tier: int) -> int:
     """Whole images per 128-row chunk of the conv WGRAD kernel (gemm3.hip g3_conv_wgrad_kernel):
     min(128 // (OH*OW), patch capacity // (H*W*Cs)) when that is >= 2, else 1 (per-image pixel tiles)."""
@@ -454,6 +472,14 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             if cfg is not None:
                 nt = 1 if N <= 16 else (2 if N <= 32 else 4)
                 v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
+        if mode == MODE_DGRAD and v is None:
+            vr = dgrad_as_fwd_conv(r)
+            if vr is not None:
+                cfg = conv_lds_config(vr, N)
+                if cfg is not None:
+                    r = vr
+                    nt = 1 if N <= 16 else (2 if N <= 32 else 4)
+                    v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
         if mode == MODE_WGRAD and v is None:
             cfg = conv_wgrad_config(r, M)
             if cfg is not None:
@@ -473,7 +499,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 nb = -(-nrows // per)
                 tl.append(np.stack([np.full(nb, p), np.arange(nb), np.zeros(nb, int), np.zeros(nb, int)], 1))
             tiles = np.concatenate(tl).astype(np.int32)
-        elif 2000 <= v < 3000 and mode == MODE_FWD:
+        elif 2000 <= v < 3000 and mode in (MODE_FWD, MODE_DGRAD):
             nt, rt = v % 10, (v // 10) % 10
             tm, bn = 64 * rt, 16 * nt
             tl = []
@@ -600,6 +626,7 @@ _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # per grouped launch
 # 96-row f tile for 64 < F <= 96: opt-in, measured slower (population B step 19.9 -> 29.1 ms: the
 # 96-row blocks drop to 2 waves per SIMD and stage 4 A passes per step; profiles/r2e/ab_wgrad96.txt)
+_DGRAD_HALO = _os.environ.get("SERANN_DGRAD_HALO", "0") == "1"   # DGRAD of stride-1 convs on the halo kernel
 _WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "0") == "1"
 _WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))

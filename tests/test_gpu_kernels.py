@@ -149,6 +149,33 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     assert _rel(dw, ref_dw) < 2e-5
 
 
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[5] * s[6] > 1 and s[7] == 1 and s[8] == 1])
+@pytest.mark.parametrize("accum", [False, True])
+def test_dgrad_as_padded_fwd_conv(shape, accum, monkeypatch):
+    """Opt-in DGRAD path (SERANN_DGRAD_HALO=1): a stride-1 conv's DGRAD as a FWD-halo conv of the
+    virtually zero-padded dZ with flipped, transposed weights (GF_VPAD), with and without GF_ACCUM."""
+    monkeypatch.setattr(H, "_DGRAD_HALO", True)
+    B, Hh, Ww, C, Fo, KH, KW, SH, SW, _ = shape
+    OH, OW = Hh - KH + 1, Ww - KW + 1
+    g = torch.Generator(device=DEV).manual_seed(1)
+    w = (torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16()
+    dz = torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16()
+    wr = w.float().permute(0, 3, 1, 2)
+    ref = ref_conv2d_input((B, C, Hh, Ww), wr, dz.float().permute(0, 3, 1, 2), (1, 1)).permute(0, 2, 3, 1)
+    dx = torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16() if accum else \
+        torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
+    if accum:
+        ref = ref + dx.float()
+    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=1, SW=1)
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    rows = [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C, K=KH * KW * Fo,
+                 flags=H.GF_ACCUM if accum else 0, **geo)]
+    plans = H.gemm3_plan(H.MODE_DGRAD, [dict(r) for r in rows], [(B * Hh * Ww, C, KH * KW * Fo)])
+    assert all(2000 <= v < 3000 for v, _, _ in plans)          # took the halo kernel
+    _run_gemm(H.MODE_DGRAD, rows, [(B * Hh * Ww, C, KH * KW * Fo)], "v3")
+    assert _rel(dx.float(), ref) < 6e-3
+
+
 def test_tiled_fwd_split_k_with_finalize():
     """Merged-Dense FWD with a long reduction: k split over blocks (fp32 partials in a workspace),
     then the grouped finalize (sum of splits + bias + activation) -- the engine's GF_SPLITWS path."""
