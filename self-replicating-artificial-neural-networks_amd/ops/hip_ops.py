@@ -264,6 +264,10 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
             # instead of a full 64-row tile plus a mostly empty second one (X read once, 25 % fewer MFMAs)
             return 96 * 1000 + 64 + (1000000 if im2col_gen else 0)
 
+        if bmf == 64 and _WGRAD_TAIL32 and (64 < M <= 96 or 128 < M <= 160):
+            # a last 64-row f tile that would be mostly empty: 32-row tiles compute 96 / 160 rows
+            # instead of 128 / 192 (at the cost of more re-reads of the X panel)
+            bmf = 32
         if bmf == 16:
             bnk = 256 if N > 128 else (128 if N > 64 else 64)
         else:
@@ -627,6 +631,9 @@ WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # p
 # 96-row f tile for 64 < F <= 96: opt-in, measured slower (population B step 19.9 -> 29.1 ms: the
 # 96-row blocks drop to 2 waves per SIMD and stage 4 A passes per step; profiles/r2e/ab_wgrad96.txt)
 _DGRAD_HALO = _os.environ.get("SERANN_DGRAD_HALO", "0") == "1"   # DGRAD of stride-1 convs on the halo kernel
+# 32-row f tiles for F in (64, 96] / (128, 160] (fewer computed rows, more X re-reads): opt-in, measured
+# slower (population B step 20.0 -> 20.5 ms, 593 -> 615 launches; profiles/r2e/ab_wgrad_tail32.txt)
+_WGRAD_TAIL32 = _os.environ.get("SERANN_WGRAD_TAIL32", "0") == "1"
 _WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "0") == "1"
 _WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
