@@ -58,13 +58,16 @@ def main():
     for ns in a.streams.split(","):
         os.environ["SERANN_STREAMS"] = ns
         cfg = TrainConfig(epochs=a.epochs, batch_size=750, val_every_epoch=False)
+        torch.cuda.synchronize()
+        ti = time.perf_counter()
         eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
         torch.cuda.synchronize()
+        init_s = time.perf_counter() - ti
         t0 = time.perf_counter()
         fit = eng.fit(data, cfg)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        print(f"streams={ns} organisms={len(irs)} steps={fit.steps} plan_s={eng.timings['plan_s']:.3f} "
+        print(f"streams={ns} organisms={len(irs)} steps={fit.steps} init_s={init_s:.3f} plan_s={eng.timings['plan_s']:.3f} "
               f"loop_s={fit.learning_time:.3f} ms/step={1e3 * fit.learning_time / fit.steps:.2f} "
               f"launches/step={eng.timings['launches_per_step']} fit_wall={wall:.2f}", flush=True)
         eng.close()
