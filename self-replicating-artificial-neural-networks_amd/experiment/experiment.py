@@ -81,7 +81,10 @@ class Experiment:
             print(*a, flush=True)
 
     def _new_ids(self, n: int) -> List[str]:
-        return [str(uuid.UUID(bytes=self._rng.bytes(16), version=4)) for _ in range(n)]
+        # one draw of 16 n bytes: RandomState.bytes draws whole 32-bit words, so this is the same byte
+        # stream (and RNG state afterwards) as n draws of 16 bytes
+        raw = self._rng.bytes(16 * n) if n > 0 else b""
+        return [str(uuid.UUID(bytes=raw[16 * k:16 * k + 16], version=4)) for k in range(n)]
 
     def execute(self, max_generations: Optional[int] = None,
                 on_generation: Optional[Callable[[int, dict], None]] = None):
@@ -275,9 +278,12 @@ class Experiment:
         if strategy is None:
             raise ValueError("Unknown offspring selection strategy")
         offspring_ids, parent_ids, genotypes = [], [], []
+        # column dicts: per-cell DataFrame.at lookups cost ~10 us each (thousands per generation at pop 1000)
+        geno_of = dict(zip(current.index, current["genotype"].values))
+        num_of = dict(zip(current.index, current["num_offspring"].values))
         for parent_id, pool in offspring_by_id.items():
-            parent_genotype = np.asarray(current.at[parent_id, "genotype"], dtype=np.float64)
-            num = int(current.at[parent_id, "num_offspring"])
+            parent_genotype = np.asarray(geno_of[parent_id], dtype=np.float64)
+            num = int(num_of[parent_id])
             pool = np.round(np.clip(pool, 0, 1))
             selected = strategy(parent_genotype, num, pool)
             selected = self._probabilistic_proofreading(parent_genotype, selected)
@@ -293,11 +299,12 @@ class Experiment:
                 nxt[c] = []
             return nxt
         off = np.stack(genotypes)
-        par = np.stack([np.asarray(current.at[i, "genotype"], np.float64) for i in parent_ids])
+        par = np.stack([np.asarray(geno_of[i], np.float64) for i in parent_ids])
         nxt["genotype_euclidean_distance_from_parent"] = np.sqrt(np.sum((off - par) ** 2, axis=1))
         nxt["genotype_hamming_distance_from_parent"] = (par != off).sum(axis=1) / self._parameters["genotype_size"]
         if self._comm.is_root:
-            parent_src = [current.at[i, "source_code"] for i in parent_ids]
+            src_of = dict(zip(current.index, current["source_code"].values))
+            parent_src = [src_of[i] for i in parent_ids]
             nxt["source_code_levenshtein_distance_from_parent"] = levenshtein_batch(list(source_code), parent_src)
         else:
             nxt["source_code_levenshtein_distance_from_parent"] = np.nan   # only rank 0 writes the DB
