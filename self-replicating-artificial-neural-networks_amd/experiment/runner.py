@@ -28,13 +28,19 @@ def default_device(comm: Comm):
 
 
 def default_engine(device: str) -> str:
+    """CPU: the torch engine.  GPU: the HIP engine, and a loud error when its extension is missing --
+    a silent eager fallback would report eager-PyTorch numbers as the framework's (the torch engine on
+    a GPU stays available explicitly: ``--engine torch`` / ``SERANN_ENGINE=torch``)."""
     if not str(device).startswith("cuda"):
         return "torch"
-    try:
-        from ..ops import hip_ops  # noqa: F401
-        return "hip" if hip_ops.available() else "torch"
-    except Exception:
-        return "torch"
+    forced = os.environ.get("SERANN_ENGINE")
+    if forced:
+        return forced
+    from ..ops import hip_ops
+    if not hip_ops.available():
+        raise RuntimeError("serann_hip extension not loadable on a GPU device: build it in-tree first "
+                           "(python -c 'import __graft_entry__ as g; g.build()'), or pass --engine torch")
+    return "hip"
 
 
 def build_codec(parameters: dict, codec: str = "auto", table_size: int = 4096, seed: int = 0,
