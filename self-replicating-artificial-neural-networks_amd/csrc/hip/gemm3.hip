@@ -1841,6 +1841,10 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     }
     bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
     const bool accum = (flags & GF_ACCUM) != 0;
+    // GF_EPI_DACT: the output is the producer's dZ = dX * act'(Y) (single writer: never with accum)
+    const bool edact = MODE == MODE_DGRAD && (flags & GF_EPI_DACT) != 0;
+    const bf16_t* __restrict__ ye = reinterpret_cast<const bf16_t*>(d.bias);
+    const int eact = (flags >> 10) & 3;
     if (n0 == 0 && N <= BN) {
         // the block's rows [m0, m0 + nrows) x all N columns are one contiguous range of the output
         bf16_t* st = lds;                            // k loop done (last barrier above)
@@ -1868,11 +1872,18 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(p.h[e]));
             }
+            if (edact) {
+                Frag yv;
+                yv.u = *reinterpret_cast<const uint4*>(&ye[(int64_t)m0 * N + v * 8]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) * act_grad_from_y(bf2f(yv.h[e]), eact));
+            }
             *reinterpret_cast<uint4*>(&dst[v * 8]) = f.u;
         }
         for (int e = nvec * 8 + t; e < total; e += 256) {
             float v = bf2f(st[e]);
             if (accum) v += bf2f(dst[e]);
+            if (edact) v = bf2f(f2bf(v)) * act_grad_from_y(bf2f(ye[(int64_t)m0 * N + e]), eact);
             dst[e] = f2bf(v);
         }
         return;
@@ -1907,6 +1918,11 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
                 for (int e = 0; e < 8; ++e)
                     if (e < nv) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(o[g + e]));
+            }
+            if (edact) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (e < nv) f.h[e] = f2bf(bf2f(f.h[e]) * act_grad_from_y(bf2f(ye[g + e]), eact));
             }
             if (nv == 8 && (g & 7) == 0) {
                 *reinterpret_cast<uint4*>(o + g) = f.u;

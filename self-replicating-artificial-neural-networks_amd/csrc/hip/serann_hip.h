@@ -33,6 +33,9 @@ enum GemmFlags : int64_t {
     GF_VPAD = 256,        // FWD halo conv kernel: the input is dZ of a stride-1 conv, virtually zero-padded by
                           // (KH-1, KW-1) on every side (H, W are the padded extents) and the weights are the
                           // transposed Wt[C][KH][KW][F] read with flipped taps: a DGRAD computed as a FWD conv
+    GF_EPI_DACT = 512,    // DGRAD (LDS-tiled kernel): out = result * act'(Y), Y = bf16 [M][N] at desc.bias, act code in
+                          // flags bits 10-11 -- the consumer writes its producer's dZ (a concat K slice whose
+                          // producing Dense has no other consumer)
     GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
                           // into a zeroed output, the bias added by the split that starts at k = 0
 };

@@ -1051,6 +1051,42 @@ class HipPopulationEngine(PopulationEngine):
                             and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
                         dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
 
+        # A Dense (relu / sigmoid) whose only consumer is a fused concat read by a single GEMM: that
+        # GEMM's K-slice DGRAD (LDS-tiled kernel) writes the Dense's dZ = dX * act'(Y) in its epilogue
+        # (GF_EPI_DACT), so the Dense's WGRAD / DGRAD read dZ alone instead of dY and Y
+        # Opt-in (SERANN_FOLD_CONCAT_ACT=1): measured neutral on population B (step 19.85 vs 19.93 ms; the
+        # slice DGRAD's extra Y read cost what the producer's WGRAD / DGRAD saved; profiles/r2e/ab_concat_act_fold.txt)
+        epi_fold = [dict() for _ in range(P)]          # concat input id -> act code
+        if os.environ.get("SERANN_FOLD_CONCAT_ACT", "0") == "1" and "tiled" not in H._OFF:
+            for o, lay in org_iter():
+                ir = lay.ir
+                rec = mem["orgs"][o]
+                owner = rec["owner"]
+                uses: Dict[int, int] = {}
+                for n in ir.nodes:
+                    if n.op == "reshape":
+                        continue
+                    for i in n.inputs:
+                        uses[owner.get(i, i)] = uses.get(owner.get(i, i), 0) + 1
+                for cid, parts in fcat[o].items():
+                    cons = [g for g, c in fcons[o].items() if c == cid]
+                    if len(cons) != 1:
+                        continue
+                    cn = ir.node(cons[0])
+                    fc = ir.num_classes + ir.genotype_size if cn.attrs["kind"] == "head_cls" else cn.attrs["f"]
+                    if fc <= H.BK:
+                        continue                  # the slice DGRAD would not run on the LDS-tiled kernel
+                    for pid, _, _ in parts:
+                        src = ir.node(owner.get(pid, pid))
+                        if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
+                                and src.id not in rec["fused_convs"] and src.id not in rec["gc_nodes"]
+                                and src.attrs["act"] in ("relu", "sigmoid") and uses.get(src.id, 0) == 1
+                                and rec["req"].get(src.id, False) and src.id not in dz_folded[o]
+                                and target(o, pid) == src.id):
+                            dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
+                            epi_fold[o][pid] = H.ACT_CODES[src.attrs["act"]]
+        self.concat_act_folds = sum(len(f) for f in epi_fold)     # (introspection: tests)
+
         STAGES = ("dgrad", "pool", "bn", "copy")
         for d in range(maxd, 0, -1):
             ab_rows, ab_cnt = [], []
@@ -1123,8 +1159,16 @@ class HipPopulationEngine(PopulationEngine):
                                                 _bnat=wptr_bf(lay.w[n.id]) + 2 * col, _bnat_ld=D,
                                                 aux=yv, act=act, out=mem["grad"].ptr(rec["grad"][own_p]), H=Hh, W=1,
                                                 C=width, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=width, K=F)
-                                    tasks["dgrad"].append((o, own_p, lambda acc, r=base: dict(r, flags=H.GF_ACCUM if acc else 0),
-                                                           (M, width, F)))
+                                    efl = 0
+                                    if pid in epi_fold[o]:
+                                        base["bias"] = self._act_ptr(mem, o, pid, inputs)   # the producer's Y
+                                        efl = H.GF_EPI_DACT | (epi_fold[o][pid] << 10)
+
+                                    def mk(acc, r=base, e=efl):
+                                        if acc and e:
+                                            raise RuntimeError("GF_EPI_DACT slice is not the only gradient writer")
+                                        return dict(r, flags=(H.GF_ACCUM if acc else 0) | e)
+                                    tasks["dgrad"].append((o, own_p, mk, (M, width, F)))
                             continue
                         if ic is not None:
                             wg_rows.append(dict(a=dz, b=ic["buf"].data_ptr(), out=gptr(lay.w[n.id]), bias=dbias,

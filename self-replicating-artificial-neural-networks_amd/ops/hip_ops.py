@@ -44,6 +44,7 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 32, 64, 128
 GF_VPAD = 256
+GF_EPI_DACT = 512        # DGRAD on the LDS-tiled kernel: output * act'(Y at desc.bias), act code in flags bits 10-11
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -490,6 +491,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
+        if int(r.get("flags", 0)) & GF_EPI_DACT and not (7000 < v < 9000):
+            raise ValueError("GF_EPI_DACT needs the LDS-tiled DGRAD kernel (K > 32, 1x1)")
         groups.setdefault(v, []).append((r, dm))
     _merge_tiled_widths(groups)
     out = []
