@@ -197,6 +197,37 @@ def test_convpool_fusion_matches_unfused(name, monkeypatch):
     assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
 
 
+def test_concat_act_fold_matches_unfolded(monkeypatch):
+    """Opt-in SERANN_FOLD_CONCAT_ACT=1: the merged Dense's K-slice DGRAD writes each producing Dense's
+    dZ = dX * act'(Y) in its epilogue (GF_EPI_DACT) and the producers' WGRAD run with act = 0.  Same
+    roundings as the unfolded path: logits and every gradient agree up to atomic-order noise."""
+    from serann.engine import hip_engine as he
+    src = ("X_layer=Dense(units=40,activation='relu')(X_layer)\n"
+           "g_layer=Dense(units=24,activation='sigmoid')(g_layer)\n"
+           "con=concatenate([Reshape((1,-1))(X_layer),Reshape((1,-1))(g_layer)])\n"
+           "con=Dense(units=64,activation='relu')(con)\n"
+           "loss_balance=0.6")
+    ir = interpret(src)
+    params = init_params(ir, 5)
+    x, g, y = _batch(80, seed=4)
+    monkeypatch.setenv("SERANN_FOLD_CONCAT_ACT", "1")
+    on = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    go, mo = on.debug_train_step(x, g, y)
+    assert on.concat_act_folds == 2
+    monkeypatch.setenv("SERANN_FOLD_CONCAT_ACT", "0")
+    off = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, mp = off.debug_train_step(x, g, y)
+    assert off.concat_act_folds == 0
+    assert _rel(on.debug_logits()[0], off.debug_logits()[0]) < 1e-3
+    a, b = on.export_arena(0, go), off.export_arena(0, gp)
+    for nid in a:
+        for k in a[nid]:
+            if np.linalg.norm(b[nid][k]) < 1e-4:
+                continue
+            assert _rel(a[nid][k], b[nid][k]) < 1e-2, (nid, k, _rel(a[nid][k], b[nid][k]))
+    assert np.allclose(mo, mp, rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("name", [n for n in sorted(ARCHS) if n.startswith("gchain") or n == "convpool_bench_a"])
 def test_gchain_fusion_matches_unfused(name, monkeypatch):
     """Fused genotype chain Conv1D(raw genotype) -> Dense -> [BatchNormalization] (gchain.hip: the chain
