@@ -28,7 +28,7 @@ def launch_bytes(la, H):
         return 0.0, []
     raw = la.descs.cpu().numpy().tobytes()
     tot, probs = 0.0, []
-    if la.kind in ("gemm", "gemm2", "gemm3"):
+    if la.kind == "gemm3":
         mode = la.arg[0] if isinstance(la.arg, tuple) else la.arg
         for r in np.frombuffer(raw, dtype=H.GEMM_DTYPE):
             M, N, K = int(r["M"]), int(r["N"]), int(r["K"])
@@ -108,7 +108,7 @@ def main():
     gb = torch.randint(0, 2, (B, 100), device=dev).bfloat16()
     yb = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
     eng._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
-    metrics = torch.zeros(len(irs), 4, device=dev)
+    metrics = torch.zeros(len(irs), 4, dtype=torch.int64, device=dev)
     inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in irs]
     plan = eng._build_plan("train", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * len(irs), metrics)
     # one full step to initialise
@@ -135,7 +135,7 @@ def main():
             ts.append(time.perf_counter() - t0)
         cls = ""
         nbytes, probs = launch_bytes(la, H)
-        if la.kind in ("gemm", "gemm2", "gemm3"):
+        if la.kind == "gemm3":
             d = np.frombuffer(la.descs.cpu().numpy().tobytes(), dtype=H.GEMM_DTYPE)
             kinds = set()
             for r in d:
@@ -146,7 +146,7 @@ def main():
                 else:
                     kinds.add("dense")
             cls = "+".join(sorted(kinds))
-            mode = la.arg[0] if la.kind in ("gemm2", "gemm3") else la.arg
+            mode = la.arg[0]
             flops = float(sum(2.0 * r["M"] * r["N"] * r["K"] for r in d))
         else:
             flops = 0.0

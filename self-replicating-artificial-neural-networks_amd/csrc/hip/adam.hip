@@ -1,11 +1,12 @@
-// Fused multi-tensor Keras-Adam over a flat fp32 parameter arena (K13 / K38).
+// Fused multi-tensor Keras-Adam over a flat fp32 parameter arena (K13 / K38).  The gradients arrive in
+// the deterministic Q32 fixed-point arena (common.h fx_*: int64, 2^-32 units) and are converted here.
 //
 // TF ResourceApplyAdam semantics (experiment_worker.py:80): lr_t = lr*sqrt(1-b2^t)/(1-b1^t),
 // m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr_t m / (sqrt(v) + eps).
 // One launch per training step for the whole population shard; the step counter and lr_t live in
 // device memory so the launch can be captured once in a hipGraph and replayed every step.  The
 // kernel also refreshes the bf16 compute copy of the weights and zeroes the gradient arena for the
-// next step's split-K / atomic accumulation.  Pure HBM streaming: 4x float4 in, 4x float4 + bf16 out.
+// next step's atomic accumulation.  Pure HBM streaming: 3x float4 + 2x int64x2 in, the same + bf16 out.
 #include "common.h"
 #include "serann_hip.h"
 
@@ -15,7 +16,7 @@ __global__ void adam_scalars_kernel(int* step, float* lr_t, float lr, float b1, 
     *lr_t = lr * sqrtf(1.f - powf(b2, (float)t)) / (1.f - powf(b1, (float)t));
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long long* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pbf, const float* __restrict__ lr_t_ptr,
                                                    int64_t n, float b1, float b2, float eps) {
@@ -24,7 +25,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 pv = reinterpret_cast<float4*>(p)[i];
-        float4 gv = reinterpret_cast<float4*>(g)[i];
+        const longlong2 g01 = reinterpret_cast<longlong2*>(g)[2 * i];
+        const longlong2 g23 = reinterpret_cast<longlong2*>(g)[2 * i + 1];
+        float4 gv = make_float4(fx_f(g01.x), fx_f(g01.y), fx_f(g23.x), fx_f(g23.y));
         float4 mv = reinterpret_cast<float4*>(m)[i];
         float4 vv = reinterpret_cast<float4*>(v)[i];
         float* pp = &pv.x; float* gg = &gv.x; float* mm = &mv.x; float* vvv = &vv.x;
@@ -40,16 +43,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
         reinterpret_cast<float4*>(p)[i] = pv;
         reinterpret_cast<float4*>(m)[i] = mv;
         reinterpret_cast<float4*>(v)[i] = vv;
-        reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        reinterpret_cast<longlong2*>(g)[2 * i] = make_longlong2(0, 0);
+        reinterpret_cast<longlong2*>(g)[2 * i + 1] = make_longlong2(0, 0);
         reinterpret_cast<ushort4*>(pbf)[i] = ob;
     }
     // tail
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        float gg = g[i];
+        float gg = fx_f(g[i]);
         float mm = b1 * m[i] + (1.f - b1) * gg;
         float vv = b2 * v[i] + (1.f - b2) * gg * gg;
         float pp = p[i] - lr_t * mm / (sqrtf(vv) + eps);
-        m[i] = mm; v[i] = vv; p[i] = pp; g[i] = 0.f; pbf[i] = f2bf(pp);
+        m[i] = mm; v[i] = vv; p[i] = pp; g[i] = 0; pbf[i] = f2bf(pp);
     }
 }
 
@@ -66,7 +70,7 @@ void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, u
     int64_t blocks = ((n >> 2) + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, as_ptr<float>(p), as_ptr<float>(g),
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, as_ptr<float>(p), as_ptr<long long>(g),
                        as_ptr<float>(m), as_ptr<float>(v), as_ptr<bf16_t>(pbf), as_ptr<const float>(lr_t), n, b1, b2,
                        eps);
     SERANN_CHECK(hipGetLastError());

@@ -1,5 +1,5 @@
 // Auxiliary grouped kernels for the SeRANN population engine:
-//   gather_batch (K14), act_bwd + bias grad (K04/K09 epilogue backward), fused BatchNormalizationF16
+//   gather_batch (K14), DGRAD weight transposes, fused BatchNormalizationF16
 //   train/infer/backward (K05/K06), maxpool fwd/bwd (K03), concat copies (K08), fused heads loss
 //   (softmax-CE + sigmoid-MSE + accuracy + dlogits, K10/K11/K12/K17), popstats (K20-K22).
 // Grouped kernels take a descriptor array and an int2 tile table (problem, chunk).
@@ -37,11 +37,11 @@ __global__ void memset32_kernel(uint32_t* p, int64_t n) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Channel-strided reduction layout shared by act_bwd and BatchNormalization (data [R][C] row-major):
+// Channel-strided reduction layout of the wide-channel (C > 256) BatchNormalization (data [R][C] row-major):
 // a block owns a chunk of rows; for C <= 256 its 256 threads are arranged as (256/C) row lanes x C
 // channel lanes, so every thread keeps ONE channel for the whole chunk (parameters in registers, no
 // per-element division, no atomics in the loop); per-channel partials are combined through LDS and
-// leave the block as one global atomic per channel.  For C > 256 threads stride over channels.
+// leave the block as one fixed-point atomic per channel.  For C > 256 threads stride over channels.
 constexpr int RED_ELEMS = 16384;   // elements per block (chunk rows = max(1, RED_ELEMS / C))
 
 struct ChanMap {
@@ -71,80 +71,18 @@ __device__ __forceinline__ ChanMap chan_map(int C) {
 
 __device__ __forceinline__ int chunk_rows(int C) { return max(1, RED_ELEMS / max(C, 1)); }
 
-// Reduce per-thread channel partials (v0, v1) for channel c0 (C <= 256 layout) into global ws.
-__device__ __forceinline__ void flush_partials(float* s0, float* s1, float v0, float v1, const ChanMap& m, int C,
-                                               float* g0, float* g1) {
-    const int t = threadIdx.x;
-    s0[t] = m.active ? v0 : 0.f;
-    if (g1) s1[t] = m.active ? v1 : 0.f;
-    __syncthreads();
-    if (t < C) {
-        float a = 0.f, b = 0.f;
-        for (int k = t; k < m.rstride * C; k += C) {
-            a += s0[k];
-            if (g1) b += s1[k];
-        }
-        atomicAdd(&g0[t], a);
-        if (g1) atomicAdd(&g1[t], b);
-    }
-    __syncthreads();
-}
-
-// dz = dy * act'(y);  dbias += column sums of dz.
-__global__ __launch_bounds__(256) void act_bwd_kernel(const ActBwdDesc* __restrict__ descs,
-                                                      const int2* __restrict__ tiles) {
-    __shared__ float s0[256];
-    const int2 td = tiles[blockIdx.x];
-    const ActBwdDesc& d = descs[td.x];
-    const int M = (int)d.M, N = (int)d.N, act = (int)d.act;
-    const bool write = d.flags & 1;
-    const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
-    const bf16_t* __restrict__ y = reinterpret_cast<const bf16_t*>(d.y);
-    bf16_t* __restrict__ dz = reinterpret_cast<bf16_t*>(d.dz);
-    float* dbias = reinterpret_cast<float*>(d.dbias);
-    const int rows = chunk_rows(N);
-    const int r0 = td.y * rows, r1 = min(M, r0 + rows);
-    const ChanMap m = chan_map(N);
-    if (N <= 256) {
-        float acc = 0.f;
-        if (m.active) {
-            const int c = m.c0;
-            for (int r = r0 + m.rlane; r < r1; r += m.rstride) {
-                const int64_t off = (int64_t)r * N + c;
-                float g = bf2f(dy[off]);
-                if (act != ACT_LINEAR) g *= act_grad_from_y(bf2f(y[off]), act);
-                if (write) dz[off] = f2bf(g);
-                acc += g;
-            }
-        }
-        if (dbias) flush_partials(s0, nullptr, acc, 0.f, m, N, dbias, nullptr);
-    } else {
-        for (int c = m.c0; c < N; c += m.cstride) {
-            float acc = 0.f;
-            for (int r = r0; r < r1; ++r) {
-                const int64_t off = (int64_t)r * N + c;
-                float g = bf2f(dy[off]);
-                if (act != ACT_LINEAR) g *= act_grad_from_y(bf2f(y[off]), act);
-                if (write) dz[off] = f2bf(g);
-                acc += g;
-            }
-            if (dbias) atomicAdd(&dbias[c], acc);
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // BatchNormalizationF16 (channel-last, rows x C).  Phases:
 //   0: ws[c] += sum (x - K_c), ws[C+c] += sum (x - K_c)^2 with the shift K_c = x[0][c]
 //      (one pass, shifted sums keep the variance accurate when |mean| >> std)
 //   2: train apply (+ moving statistics, saved mean / invstd)      3: inference apply
 //   4: ws2[c] += sum dy, ws2[C+c] += sum dy*xhat                      5: backward apply (+ dgamma, dbeta)
-__device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const float* ws, int c, float& mu,
+__device__ __forceinline__ void bn_stats(const BnDesc& d, int C, float R, const long long* ws, int c, float& mu,
                                          float& var) {
     const float K = bf2f(reinterpret_cast<const bf16_t*>(d.x)[c]);
-    const float m1 = ws[c] / R;
+    const float m1 = fxw_sum<1>(ws, C, c) / R;
     mu = K + m1;
-    var = fmaxf(ws[C + c] / R - m1 * m1, 0.f);
+    var = fmaxf(fxw_sum<1>(ws, C, C + c) / R - m1 * m1, 0.f);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -167,15 +105,14 @@ __host__ __device__ __forceinline__ int bn_stat_mult(int nsr, int srb1) {
     return (nsr + srb1 - 1) / srb1 < BN_STAT_SMALL ? 1 : BN_RED_MULT;
 }
 
-// Statistics workspace of the vectorised path: BN_WS_STRIPES copies of the 2C sums; block `tile` adds
-// into copy tile % BN_WS_STRIPES (an eighth of the same-address atomics: they serialise in L2 and
-// bounded the statistics phases), readers sum the copies.  Producers fused into other kernels
-// (GF_BNSTAT, gemm3.hip) stripe the same way, by their own blockIdx.x % BN_WS_STRIPES.
-__device__ __forceinline__ float wsum(const float* ws, int C, int idx) {
-    float v = 0.f;
-#pragma unroll
-    for (int s = 0; s < BN_WS_STRIPES; ++s) v += ws[s * 2 * C + idx];
-    return v;
+// Statistics workspace of the vectorised path: BN_WS_STRIPES copies of the 2C wide fixed-point sums
+// (common.h fxw_*); block `tile` adds into copy tile % BN_WS_STRIPES (an eighth of the same-address
+// atomics: they serialise in L2 and bounded the statistics phases), readers sum the copies in integer
+// arithmetic -- the result does not depend on the order of the atomics (deterministic training).
+// Producers fused into other kernels (GF_BNSTAT, gemm3.hip; gchain.hip) stripe the same way, by their own
+// blockIdx.x % BN_WS_STRIPES.
+__device__ __forceinline__ float wsum(const long long* ws, int C, int idx) {
+    return fxw_sum<BN_WS_STRIPES>(ws, C, idx);
 }
 
 template <int phase>
@@ -196,8 +133,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
     const int sr0 = tile * srb, sr1 = min(nsr, sr0 + srb);
     const int64_t total = (int64_t)R * C;
     const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
-    float* ws = reinterpret_cast<float*>(d.ws);
-    float* wsw = ws + (tile % BN_WS_STRIPES) * 2 * C;     // this block's statistics copy
+    const long long* ws = reinterpret_cast<const long long*>(d.ws);
+    long long* wsw = reinterpret_cast<long long*>(d.ws) + (tile % BN_WS_STRIPES) * 4 * C;   // this block's copy
     int ch[8];
     {
         int c = (8 * i) % C;
@@ -302,8 +239,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
     }
     if (phase == 5 && tile == 0) {
         for (int c = t; c < C; c += 256) {
-            if (flags & 1) reinterpret_cast<float*>(d.dgamma)[c] += wsum(ws, C, C + c);
-            if (flags & 2) reinterpret_cast<float*>(d.dbeta)[c] += wsum(ws, C, c);
+            if (flags & 1) reinterpret_cast<long long*>(d.dgamma)[c] += fx_q(wsum(ws, C, C + c));   // Q32 arena
+            if (flags & 2) reinterpret_cast<long long*>(d.dbeta)[c] += fx_q(wsum(ws, C, c));
         }
     }
     __syncthreads();
@@ -394,8 +331,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
             for (int s = t; s < 2048; s += 256) { a += r0[s]; b += r1[s]; }
             for (int o = C; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
             if (lane < C) {
-                atomicAdd(&wsw[lane], a);
-                atomicAdd(&wsw[C + lane], b);
+                fxw_add(wsw + 2 * lane, a);
+                fxw_add(wsw + 2 * (C + lane), b);
             }
             return;
         }
@@ -407,8 +344,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
                     a += r0[g * 8 * C + c + k * C];
                     b += r1[g * 8 * C + c + k * C];
                 }
-            atomicAdd(&wsw[c], a);
-            atomicAdd(&wsw[C + c], b);
+            fxw_add(wsw + 2 * c, a);
+            fxw_add(wsw + 2 * (C + c), b);
         }
     }
 }
@@ -429,7 +366,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
     const int flags = (int)d.flags;
     const float eps = (float)d.eps;
     const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
-    float* ws = reinterpret_cast<float*>(d.ws);
+    long long* ws = reinterpret_cast<long long*>(d.ws);     // one wide copy (C > 256: no stripes)
     const float* gamma = reinterpret_cast<const float*>(d.gamma);
     const float* beta = reinterpret_cast<const float*>(d.beta);
     float* mean = reinterpret_cast<float*>(d.mean);
@@ -466,7 +403,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
                 b += v * v;
             }
             if (C <= 256) { s0[threadIdx.x] = a; s1[threadIdx.x] = b; }
-            else { atomicAdd(&ws[c], a); atomicAdd(&ws[C + c], b); }
+            else { fxw_add(ws + 2 * c, a); fxw_add(ws + 2 * (C + c), b); }
         } else if (phase == 4) {
             const float mu = mean[c], is = invstd[c];
             const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
@@ -478,7 +415,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
                 b += g * (bf2f(x[off]) - mu) * is;
             }
             if (C <= 256) { s0[threadIdx.x] = a; s1[threadIdx.x] = b; }
-            else { atomicAdd(&ws[c], a); atomicAdd(&ws[C + c], b); }
+            else { fxw_add(ws + 2 * c, a); fxw_add(ws + 2 * (C + c), b); }
         } else if (phase == 2 || phase == 3) {
             float mu, is;
             if (phase == 2) {
@@ -498,15 +435,15 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
             }
         } else {   // phase 5
             if (td.y == 0 && rl == 0) {
-                float* dg = reinterpret_cast<float*>(d.dgamma);
-                float* db = reinterpret_cast<float*>(d.dbeta);
-                if (flags & 1) dg[c] += ws[C + c];
-                if (flags & 2) db[c] += ws[c];
+                long long* dg = reinterpret_cast<long long*>(d.dgamma);
+                long long* db = reinterpret_cast<long long*>(d.dbeta);
+                if (flags & 1) dg[c] += fx_q(fxw_sum<1>(ws, C, C + c));
+                if (flags & 2) db[c] += fx_q(fxw_sum<1>(ws, C, c));
             }
             if (flags & 8) continue;
             const float mu = mean[c], is = invstd[c];
             const float gg = ((flags & 1) ? gamma[c] : 1.f) * is;
-            const float a = ws[c] / Rf, b = ws[C + c] / Rf;
+            const float a = fxw_sum<1>(ws, C, c) / Rf, b = fxw_sum<1>(ws, C, C + c) / Rf;
             const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
             bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
             for (int r = r0 + rl; r < r1; r += rs) {
@@ -524,8 +461,8 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
         if (threadIdx.x < C) {
             float a = 0.f, b = 0.f;
             for (int k = threadIdx.x; k < m.rstride * C; k += C) { a += s0[k]; b += s1[k]; }
-            atomicAdd(&ws[threadIdx.x], a);
-            atomicAdd(&ws[C + threadIdx.x], b);
+            fxw_add(ws + 2 * threadIdx.x, a);
+            fxw_add(ws + 2 * (C + threadIdx.x), b);
         }
     }
 }
@@ -699,7 +636,8 @@ __global__ __launch_bounds__(256) void copy2d_kernel(const CopyDesc* __restrict_
 // Fused heads loss: one wave per sample row.  logits fp32 [B][NC+L] (classification logits then
 // replication logits), labels int [B], target bf16 [B][L].  Train: writes dlogits bf16 (d(lb*CE +
 // (1-lb)*MSE)/dz, Keras mean reduction over the batch) and accumulates metrics[0]+=loss,
-// metrics[1]+=correct, metrics[2]+=sum_row mean_j (sigmoid-g)^2, metrics[3]+=rows.
+// metrics[1]+=correct, metrics[2]+=sum_row mean_j (sigmoid-g)^2, metrics[3]+=rows (int64 Q32 fixed point,
+// common.h: the sums do not depend on the order of the blocks' atomics).
 constexpr int LOSS_ROWS = 64;   // rows per block (16 per wave); metrics reduced per block
 
 __global__ __launch_bounds__(256) void loss_kernel(const LossDesc* __restrict__ descs, int train, int nvalid) {
@@ -758,7 +696,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const LossDesc* __restrict__ 
     __syncthreads();
     if (threadIdx.x < 4) {
         const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        if (v != 0.f) atomicAdd(reinterpret_cast<float*>(d.metrics) + threadIdx.x, v);
+        if (v != 0.f) fx_add(reinterpret_cast<long long*>(d.metrics) + threadIdx.x, v);   // Q32 (deterministic)
     }
 }
 
@@ -810,13 +748,6 @@ void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream) {
     int64_t blocks = (n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(memset32_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), as_ptr<uint32_t>(ptr), n);
-    SERANN_CHECK(hipGetLastError());
-}
-
-void launch_act_bwd(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
-    if (ntiles <= 0) return;
-    hipLaunchKernelGGL(act_bwd_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
-                       as_ptr<const ActBwdDesc>(descs), as_ptr<const int2>(tiles));
     SERANN_CHECK(hipGetLastError());
 }
 
@@ -1007,5 +938,32 @@ void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t strea
     if (ntiles <= 0) return;
     hipLaunchKernelGGL(imcol_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
                        as_ptr<const ImcolDesc>(descs), as_ptr<const int2>(tiles));
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Transposed bf16 weights for DGRAD kernels that cannot read the natural layout:
+// Wt[c][kh][kw][f] = Wm[f][kh][kw][c], grouped over problems (4096 destination elements per block).
+__global__ __launch_bounds__(256) void transpose_weights_kernel(const TransDesc* __restrict__ descs,
+                                                                const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const TransDesc& d = descs[td.x];
+    const int64_t total = d.F * d.P * d.C;
+    const bf16_t* src = reinterpret_cast<const bf16_t*>(d.src);
+    bf16_t* dst = reinterpret_cast<bf16_t*>(d.dst);
+    const int64_t e0 = (int64_t)td.y * 4096;
+    for (int64_t e = e0 + threadIdx.x; e < min(total, e0 + 4096); e += blockDim.x) {
+        const int64_t f = e % d.F;                   // e indexes the destination [c][p][f]
+        const int64_t rest = e / d.F;
+        const int64_t pp = rest % d.P;
+        const int64_t c = rest / d.P;
+        dst[e] = src[(f * d.P + pp) * d.C + c];
+    }
+}
+
+void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipLaunchKernelGGL(transpose_weights_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
+                       as_ptr<const TransDesc>(descs), as_ptr<const int2>(tiles));
     SERANN_CHECK(hipGetLastError());
 }

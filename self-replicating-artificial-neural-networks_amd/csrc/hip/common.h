@@ -45,5 +45,56 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act) {
     return 1.f;
 }
 
+// ---- deterministic accumulation -------------------------------------------------
+// Every float reduction whose partial sums meet through atomics -- WGRAD m-splits and bias gradients
+// into the gradient arena, BatchNorm statistics, the loss metrics -- accumulates in signed 64-bit fixed
+// point.  Integer addition is associative and wraps modulo 2^64, so the total is independent of the
+// order in which the atomics land (and of transient overflow): a replayed training step is bitwise
+// reproducible, and so is the population a seeded experiment evolves.
+//  * fx ("Q32", one word): the gradient arena and the loss metrics.  32 fractional bits: resolution
+//    2^-32 = 2.3e-10 absolute (below the bf16 operand noise of any gradient that can move an Adam
+//    update with eps = 1e-4), final sums within +-2^31.  Each contribution is clamped to +-2^30 first
+//    (NaN -> -2^30) so the conversion is always defined.
+//  * fxw ("wide", two words hi, lo): BatchNorm statistics (sums of squares over up to 588k rows).  A
+//    contribution q = round(v * 2^32) is split as hi = q >> 32, lo = q & (2^32 - 1) (lo >= 0); the
+//    words are summed separately, total = hi + lo * 2^-32: same resolution, range +-2^63.
+typedef unsigned long long u64_t;
+constexpr float FX_SCALE = 4294967296.f;            // 2^32
+constexpr float FX_INV = 2.3283064365386963e-10f;   // 2^-32
+
+__device__ __forceinline__ long long fx_q(float v) {
+    return llrintf(fminf(fmaxf(v, -1073741824.f), 1073741824.f) * FX_SCALE);
+}
+__device__ __forceinline__ void fx_add(long long* p, float v) {
+    atomicAdd(reinterpret_cast<u64_t*>(p), (u64_t)fx_q(v));
+}
+__device__ __forceinline__ float fx_f(long long q) { return (float)q * FX_INV; }
+
+__device__ __forceinline__ void fxw_add(long long* p, float v) {
+    long long hi, lo = 0;
+    if (fabsf(v) < 1.0e9f) {
+        const long long q = llrintf(v * FX_SCALE);
+        hi = q >> 32;
+        lo = q & 0xffffffffLL;
+    } else {                                          // |v| >= 1e9 > 2^24: already an integer (or NaN)
+        hi = (v != v) ? 0 : (long long)fminf(fmaxf(v, -9.0e18f), 9.0e18f);
+    }
+    atomicAdd(reinterpret_cast<u64_t*>(p), (u64_t)hi);
+    if (lo) atomicAdd(reinterpret_cast<u64_t*>(p + 1), (u64_t)lo);
+}
+// Sum of sum index ``idx`` over the BN_WS_STRIPES copies of a wide statistics workspace laid out as
+// [stripe][2C sums][hi, lo] (serann_hip.h BN_WS_STRIPES); integer sums first, one rounding at the end.
+template <int STRIPES>
+__device__ __forceinline__ float fxw_sum(const long long* ws, int C, int idx) {
+    long long hi = 0;
+    u64_t lo = 0;
+#pragma unroll
+    for (int s = 0; s < STRIPES; ++s) {
+        hi += ws[2 * (s * 2 * C + idx)];
+        lo += (u64_t)ws[2 * (s * 2 * C + idx) + 1];
+    }
+    return (float)((double)hi + (double)lo * (1.0 / 4294967296.0));
+}
+
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename T> static inline T* as_ptr(uint64_t p) { return reinterpret_cast<T*>(p); }

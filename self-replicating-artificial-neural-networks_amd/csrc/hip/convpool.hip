@@ -16,7 +16,7 @@
 // * WGRAD: dW[f][tap] = sum_{b,p} dz[b,p,f] [argmax == w] img[b][pos(p, w) + tap], one MFMA per
 //   (window offset, 32 pooled positions, 16 filters, 16 taps): A = dz masked by the argmax (held in
 //   registers across the window offsets), B = patches from LDS.  The bias gradient is the plain sum
-//   of dz.  Results are flushed with one fp32 atomic per (block, weight).
+//   of dz.  Results are flushed with one Q32 fixed-point atomic per (wave, weight) (deterministic).
 // There is no DGRAD: the input is the raw image.
 //
 // One block = 4 waves = one organism x a chunk of images x a group of 64 filters.  Every wave owns
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
         }
     }
     // D[row = filter][col = tap]: lane holds filters 4*kg + r of tap column col
-    float* __restrict__ dw = reinterpret_cast<float*>(d.dw);
+    long long* __restrict__ dw = reinterpret_cast<long long*>(d.dw);     // Q32 gradient arena (common.h)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
 #pragma unroll
@@ -411,11 +411,11 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int f = f0 + nt * 16 + kg * 4 + r;
-                if (f < F) atomicAdd(dw + (int64_t)f * taps + tap, acc[nt][tt][r]);
+                if (f < F) fx_add(dw + (int64_t)f * taps + tap, acc[nt][tt][r]);
             }
         }
     }
-    float* __restrict__ dbias = reinterpret_cast<float*>(d.dbias);
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.dbias);
     if (dbias != nullptr) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
             s += __shfl_xor(s, 16, 64);
             s += __shfl_xor(s, 32, 64);
             const int f = f0 + nt * 16 + col;
-            if (kg == 0 && f < F) atomicAdd(dbias + f, s);
+            if (kg == 0 && f < F) fx_add(dbias + f, s);
         }
     }
 }

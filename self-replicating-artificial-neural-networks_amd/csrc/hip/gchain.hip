@@ -21,7 +21,11 @@
 //   mode 2 BSTAT  recompute x; read dy; accumulate sum dy and sum dy * xhat (BN phase-4 workspace)
 //   mode 3 BFULL  recompute Z1 = act1(W1 * g + b1) and x; read dy; dZ2 = BN_bwd(dy) * act2'(x) in
 //                 registers; dW2 += Z1^T dZ2, db2 += sum dZ2, dZ1 = dZ2 W2 * act1'(Z1), dW1 += P^T dZ1
-//                 (P = genotype patches), db1 += sum dZ1; one fp32 atomic flush per block
+//                 (P = genotype patches), db1 += sum dZ1; one fixed-point atomic flush per block
+//
+// Determinism: the 4 waves of a block combine their partial sums in LDS in wave order
+// (barrier-separated phases, no LDS float atomics) and blocks meet in the fixed-point workspaces and
+// gradient arena of common.h (fxw_add / fx_add), so every pass is bitwise reproducible.
 //
 // MFMA orientation: the chain runs transposed, D1 = W1 * P^T ([F1][rows]) and D2 = W2 * Z1^T
 // ([F2][rows]), so each accumulator tile holds 4 consecutive channels of one row per lane and feeds
@@ -90,11 +94,8 @@ typedef __attribute__((address_space(3))) uint32_t gc_lu32;
 typedef unsigned int gc_u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) gc_u32x2 gc_lu32x2;
 
-__device__ __forceinline__ float gc_wsum(const float* ws, int C, int idx) {
-    float v = 0.f;
-#pragma unroll
-    for (int s = 0; s < BN_WS_STRIPES; ++s) v += ws[s * 2 * C + idx];
-    return v;
+__device__ __forceinline__ float gc_wsum(int64_t ws, int C, int idx) {
+    return fxw_sum<BN_WS_STRIPES>(reinterpret_cast<const long long*>(ws), C, idx);
 }
 
 // Transposed LDS read of a 16x16x32 operand fragment from an image [rows][ld]: lane (q, i) receives
@@ -323,15 +324,14 @@ __global__ __launch_bounds__(256) void gchain_fwd_kernel(const GChainDesc* __res
             }
             __syncthreads();
             const float eps = (float)d.eps, mom = (float)d.momentum;
-            const float* ws = reinterpret_cast<const float*>(d.ws);
             float* mm = reinterpret_cast<float*>(d.mm);
             float* mv = reinterpret_cast<float*>(d.mv);
             for (int c = threadIdx.x; c < F2; c += 256) {
                 float mu, var;
                 if (train) {
-                    const float m1 = gc_wsum(ws, C, c) / Rf;
+                    const float m1 = gc_wsum(d.ws, C, c) / Rf;
                     mu = sPar[2][c] + m1;
-                    var = fmaxf(gc_wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
+                    var = fmaxf(gc_wsum(d.ws, C, C + c) / Rf - m1 * m1, 0.f);
                 } else {
                     mu = mm[c];
                     var = mv[c];
@@ -409,23 +409,35 @@ __global__ __launch_bounds__(256) void gchain_fwd_kernel(const GChainDesc* __res
         }
     }
     if (MODE == 0) {
-        // rows of a lane group -> the group's lane 0; waves -> LDS; one atomic per channel and block
+        // rows of a lane group -> the group's lane 0; waves -> LDS in wave order; one fixed-point
+        // atomic per channel and block
+        float ra[T2][4], rb[T2][4];
 #pragma unroll
         for (int mt = 0; mt < T2; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float a = gc_rowsum(s1[mt][r >> 1][r & 1]), b = gc_rowsum(s2[mt][r >> 1][r & 1]);
-                const int ch = 16 * mt + 4 * q + r;
-                if ((lane & 15) == 0 && ch < F2) {
-                    atomicAdd(&sPar[0][ch], a);
-                    atomicAdd(&sPar[1][ch], b);
-                }
+                ra[mt][r] = gc_rowsum(s1[mt][r >> 1][r & 1]);
+                rb[mt][r] = gc_rowsum(s2[mt][r >> 1][r & 1]);
             }
-        __syncthreads();
-        float* wsw = reinterpret_cast<float*>(d.ws) + (blockIdx.x % BN_WS_STRIPES) * 2 * C;
+        for (int w = 0; w < 4; ++w) {
+            if (wave == w && (lane & 15) == 0) {
+#pragma unroll
+                for (int mt = 0; mt < T2; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ch = 16 * mt + 4 * q + r;
+                        if (ch < F2) {
+                            sPar[0][ch] += ra[mt][r];
+                            sPar[1][ch] += rb[mt][r];
+                        }
+                    }
+            }
+            __syncthreads();
+        }
+        long long* wsw = reinterpret_cast<long long*>(d.ws) + (blockIdx.x % BN_WS_STRIPES) * 4 * C;
         for (int c = threadIdx.x; c < F2; c += 256) {
-            atomicAdd(&wsw[c], sPar[0][c]);
-            atomicAdd(&wsw[C + c], sPar[1][c]);
+            fxw_add(wsw + 2 * c, sPar[0][c]);
+            fxw_add(wsw + 2 * (C + c), sPar[1][c]);
         }
     }
 }
@@ -525,18 +537,17 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
             sK[0][c] = is;
             sK[1][c] = -reinterpret_cast<const float*>(d.mean)[c] * is;
         } else if (bn) {
-            const float* wsb = reinterpret_cast<const float*>(d.wsb);
             const float mu = reinterpret_cast<const float*>(d.mean)[c];
             const float is = reinterpret_cast<const float*>(d.invstd)[c];
             const float gg = ((flags & GC_GAMMA) ? reinterpret_cast<const float*>(d.gamma)[c] : 1.f) * is;
-            const float sdy = gc_wsum(wsb, C, c), sdyx = gc_wsum(wsb, C, C + c);
+            const float sdy = gc_wsum(d.wsb, C, c), sdyx = gc_wsum(d.wsb, C, C + c);
             const float ma = sdy / Rf, mb = sdyx / Rf;
             sK[0][c] = gg;
             sK[1][c] = -gg * is * mb;
             sK[2][c] = -gg * (ma - mu * is * mb);
             if (td.y == 0) {
-                if (flags & GC_GAMMA) reinterpret_cast<float*>(d.dgamma)[c] += sdyx;
-                if (flags & GC_BETA) reinterpret_cast<float*>(d.dbeta)[c] += sdy;
+                if (flags & GC_GAMMA) reinterpret_cast<long long*>(d.dgamma)[c] += fx_q(sdyx);
+                if (flags & GC_BETA) reinterpret_cast<long long*>(d.dbeta)[c] += fx_q(sdy);
             }
         } else {
             sK[0][c] = 1.f;
@@ -699,28 +710,40 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
             dw1[m1] = gc_mma(a1, pp, dw1[m1]);
         }
     }
-    // ---- flush: waves -> LDS (the images are dead), one fp32 atomic per element and block ----
+    // ---- flush: waves -> LDS in wave order (the images are dead), one fixed-point atomic per element
+    // and block ----
     __syncthreads();
     gc_lf32* red = (gc_lf32*)sMem;
     if (MODE == 2) {
         for (int e = threadIdx.x; e < 2 * F2P; e += 256) red[e] = 0.f;
-        __syncthreads();
+        float ra[T2][4], rb[T2][4];
 #pragma unroll
         for (int mt = 0; mt < T2; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float a = gc_rowsum(s1[mt][r]), b = gc_rowsum(s2[mt][r]);
-                const int ch = 16 * mt + 4 * q + r;
-                if ((lane & 15) == 0 && ch < F2) {
-                    atomicAdd((float*)&red[ch], a);
-                    atomicAdd((float*)&red[F2P + ch], b);
-                }
+                ra[mt][r] = gc_rowsum(s1[mt][r]);
+                rb[mt][r] = gc_rowsum(s2[mt][r]);
             }
         __syncthreads();
-        float* wsw = reinterpret_cast<float*>(d.wsb) + (blockIdx.x % BN_WS_STRIPES) * 2 * C;
+        for (int w = 0; w < 4; ++w) {
+            if (wave == w && (lane & 15) == 0) {
+#pragma unroll
+                for (int mt = 0; mt < T2; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ch = 16 * mt + 4 * q + r;
+                        if (ch < F2) {
+                            red[ch] += ra[mt][r];
+                            red[F2P + ch] += rb[mt][r];
+                        }
+                    }
+            }
+            __syncthreads();
+        }
+        long long* wsw = reinterpret_cast<long long*>(d.wsb) + (blockIdx.x % BN_WS_STRIPES) * 4 * C;
         for (int c = threadIdx.x; c < F2; c += 256) {
-            atomicAdd(&wsw[c], red[c]);
-            atomicAdd(&wsw[C + c], red[F2P + c]);
+            fxw_add(wsw + 2 * c, red[c]);
+            fxw_add(wsw + 2 * (C + c), red[F2P + c]);
         }
         return;
     }
@@ -729,48 +752,53 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
     gc_lf32* redb2 = redb1 + F1P;
     for (int e = threadIdx.x; e < Lds::RED; e += 256) red[e] = 0.f;
     __syncthreads();
+    // every lane of a wave owns distinct LDS elements; the waves add in order 0..3 (the branch is
+    // wave-uniform, so the row-sum shuffles inside it are well defined)
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
 #pragma unroll
-    for (int m2 = 0; m2 < (MODE == 3 ? T2 : 1); ++m2)
+            for (int m2 = 0; m2 < (MODE == 3 ? T2 : 1); ++m2)
 #pragma unroll
-        for (int m1 = 0; m1 < T1; ++m1)
+                for (int m1 = 0; m1 < T1; ++m1)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                atomicAdd((float*)&red[(16 * m2 + 4 * q + r) * F1P + 16 * m1 + (lane & 15)], dw2[m2][m1][r]);
+                    for (int r = 0; r < 4; ++r) red[(16 * m2 + 4 * q + r) * F1P + 16 * m1 + (lane & 15)] += dw2[m2][m1][r];
 #pragma unroll
-    for (int m1 = 0; m1 < T1; ++m1)
+            for (int m1 = 0; m1 < T1; ++m1)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd((float*)&red1[(16 * m1 + 4 * q + r) * 16 + (lane & 15)], dw1[m1][r]);
+                for (int r = 0; r < 4; ++r) red1[(16 * m1 + 4 * q + r) * 16 + (lane & 15)] += dw1[m1][r];
 #pragma unroll
-    for (int mt = 0; mt < T1; ++mt)
+            for (int mt = 0; mt < T1; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float v = gc_rowsum(db1p[mt][r]);
-            if ((lane & 15) == 0) atomicAdd((float*)&redb1[16 * mt + 4 * q + r], v);
+                for (int r = 0; r < 4; ++r) {
+                    const float v = gc_rowsum(db1p[mt][r]);
+                    if ((lane & 15) == 0) redb1[16 * mt + 4 * q + r] += v;
+                }
+#pragma unroll
+            for (int mt = 0; mt < T2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = gc_rowsum(s1[mt][r]);
+                    if ((lane & 15) == 0) redb2[16 * mt + 4 * q + r] += v;
+                }
         }
-#pragma unroll
-    for (int mt = 0; mt < T2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float v = gc_rowsum(s1[mt][r]);
-            if ((lane & 15) == 0) atomicAdd((float*)&redb2[16 * mt + 4 * q + r], v);
-        }
-    __syncthreads();
-    float* gw2 = reinterpret_cast<float*>(d.dw2);
-    float* gw1 = reinterpret_cast<float*>(d.dw1);
-    float* gb1 = reinterpret_cast<float*>(d.db1);
-    float* gb2 = reinterpret_cast<float*>(d.db2);
+        __syncthreads();
+    }
+    long long* gw2 = reinterpret_cast<long long*>(d.dw2);     // Q32 gradient arena (common.h)
+    long long* gw1 = reinterpret_cast<long long*>(d.dw1);
+    long long* gb1 = reinterpret_cast<long long*>(d.db1);
+    long long* gb2 = reinterpret_cast<long long*>(d.db2);
     for (int e = threadIdx.x; e < F2 * F1; e += 256) {
         const int o = e / F1, i = e - o * F1;
-        atomicAdd(&gw2[e], red[o * F1P + i]);
+        fx_add(&gw2[e], red[o * F1P + i]);
     }
     for (int e = threadIdx.x; e < F1 * T; e += 256) {
         const int i = e / T, t = e - i * T;
-        atomicAdd(&gw1[e], red1[i * 16 + t]);
+        fx_add(&gw1[e], red1[i * 16 + t]);
     }
     if (gb1 != nullptr)
-        for (int c = threadIdx.x; c < F1; c += 256) atomicAdd(&gb1[c], redb1[c]);
+        for (int c = threadIdx.x; c < F1; c += 256) fx_add(&gb1[c], redb1[c]);
     if (gb2 != nullptr)
-        for (int c = threadIdx.x; c < F2; c += 256) atomicAdd(&gb2[c], redb2[c]);
+        for (int c = threadIdx.x; c < F2; c += 256) fx_add(&gb2[c], redb2[c]);
 }
 
 // ------------------------------------------------------------------------------------------------

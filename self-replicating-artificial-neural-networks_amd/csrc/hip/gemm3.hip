@@ -21,7 +21,7 @@
 //   FWD   : Y[m][f]  = act(im2col(X)[m][k] . Wm[f][k] + b[f])
 //   DGRAD : dX[m][c] = sum_{k'=(kh,kw,f)} dZ[b,(ih-kh)/SH,(iw-kw)/SW,f] . Wt[c][k']
 //   WGRAD : dWm[f][k] += sum_m dZ[m][f] . im2col(X)[m][k]      (LDS tiles, transposing LDS reads,
-//           64 rows of m per barrier pair, fp32 atomics into the gradient arena for split-m)
+//           64 rows of m per barrier pair, Q32 fixed-point atomics into the gradient arena for split-m)
 // dZ = dY * act'(Y) is formed on the fly from the layer output Y (GemmDesc::aux) in DGRAD / WGRAD.
 #include "common.h"
 #include "serann_hip.h"
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
     const int f0 = td.y * BMF, k0c = td.z * BNK;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // in units of 32 rows of m
     const int mlim = min(g.K, kt1 * 32);
-    float* __restrict__ dbias = reinterpret_cast<float*>(d.bias);
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int ohw = g.OH * g.OW;
     const int64_t nb = g.K / ohw;                              // batch
@@ -719,17 +719,17 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
             if (a_act && lane < ACH) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+                    if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
             }
         } else if (a_act) {
             // non-power-of-two chunk count (BMF = 160 / 192): one atomic per thread and f
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+                if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
         }
     }
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
-    float* out = reinterpret_cast<float*>(d.out);
+    long long* out = reinterpret_cast<long long*>(d.out);     // Q32 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
 #pragma unroll
     for (int i = 0; i < TF; ++i)
@@ -742,8 +742,8 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
                 if (row < g.M) {
                     // GF_WSTORE: this block is the problem's only m-split -> the sole writer
-                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = acc[i][j][r];
-                    else atomicAdd(out + (int64_t)row * ldo + col, acc[i][j][r]);
+                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = fx_q(acc[i][j][r]);
+                    else fx_add(out + (int64_t)row * ldo + col, acc[i][j][r]);
                 }
             }
         }
@@ -786,30 +786,12 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     const uint4 zero = make_uint4(0, 0, 0, 0);
 
     // ---- stage the patch: input rows [oh_a*SH, oh_a*SH + rows_in) of image b ----------------------
-    const bool vpad = (g.flags & GF_VPAD) != 0;
-    if (!vpad) {
+    {
         const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * g.H * g.W * g.C * 2);
         const int gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
         for (int p = t; p < npix; p += 256) {
             for (int c = 0; c < Cp; c += 8) {
                 uint4 v = bl16(rA, gbase + p * g.C + c);
-                if (c + 8 > g.C) v = splice(v, zero, g.C - c);
-                *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
-            }
-        }
-    } else {
-        // DGRAD of a stride-1 conv: the patch holds rows of dZ [B][Hr][Wr][C] zero-padded by (KH-1, KW-1)
-        // (H, W are the padded extents); padding pixels are written as zeros, never loaded
-        const int Hr = g.H - 2 * (g.KH - 1), Wr = g.W - 2 * (g.KW - 1);
-        const rsrc_t rA = mkrsrc(d.a, (int64_t)(g.M / ohw) * Hr * Wr * g.C * 2);
-        for (int p = t; p < npix; p += 256) {
-            const int lr = fdiv(p, g.dW);
-            const int rr = oh_a + lr - (g.KH - 1);
-            const int rc = p - lr * g.W - (g.KW - 1);
-            const bool in = rr >= 0 && rr < Hr && rc >= 0 && rc < Wr;
-            const int src = ((b * Hr + rr) * Wr + rc) * g.C;
-            for (int c = 0; c < Cp; c += 8) {
-                uint4 v = in ? bl16(rA, src + c) : zero;
                 if (c + 8 > g.C) v = splice(v, zero, g.C - c);
                 *reinterpret_cast<uint4*>(&patch[p * Cs + c]) = v;
             }
@@ -838,7 +820,7 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
         const int tap = fdiv(e, dCp);
         const int c = e - tap * Cp;
         if (bn >= BN || tap >= taps || c >= g.C) return zero;
-        uint4 v = bl16(rB, brow + (vpad ? taps - 1 - tap : tap) * g.C + c);   // VPAD: flipped kernel
+        uint4 v = bl16(rB, brow + tap * g.C + c);
         if (c + 8 > g.C) v = splice(v, zero, g.C - c);
         return v;
     };
@@ -966,7 +948,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const rsrc_t rX = mkrsrc(d.b, (int64_t)nbatch * g.H * g.W * g.C * 2);
     const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
-    float* __restrict__ dbias = reinterpret_cast<float*>(d.bias);
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
     const uint4 zero = make_uint4(0, 0, 0, 0);
 
     constexpr int WR = (BMF == 64) ? 2 : 1;          // waves along f
@@ -1123,12 +1105,12 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         if (lane < ACH && a_r0 < TM) {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (j < a_nv) atomicAdd(dbias + f0 + a_f + j, bsum[j]);
+                if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
         }
     }
     // flush: column k' -> (tap, c) -> dWm[f][tap*C + c] for c < C
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
-    float* out = reinterpret_cast<float*>(d.out);
+    long long* out = reinterpret_cast<long long*>(d.out);
 #pragma unroll
     for (int j = 0; j < TK; ++j) {
         const int kp = kc0 + wk * (BNK / WC) + j * 16 + c16;
@@ -1141,7 +1123,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row < g.M) atomicAdd(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                if (row < g.M) fx_add(out + (int64_t)row * g.N + col, acc[i][j][r]);
             }
     }
 }
@@ -1295,7 +1277,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
             red[(8 + j) * 256 + t] = active ? s2[j] : 0.f;
         }
         __syncthreads();
-        float* ws = reinterpret_cast<float*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 2 * N;   // stripe
+        long long* ws = reinterpret_cast<long long*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 4 * N;   // stripe
         for (int o = t; o < FC * 8; o += 256) {
             const int ch = o >> 3, j = o & 7, c = ch * 8 + j;
             if (c >= N) continue;
@@ -1304,8 +1286,8 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                 a += red[j * 256 + q * FC + ch];
                 b += red[(8 + j) * 256 + q * FC + ch];
             }
-            atomicAdd(ws + c, a);
-            atomicAdd(ws + N + c, b);
+            fxw_add(ws + 2 * c, a);
+            fxw_add(ws + 2 * (N + c), b);
         }
     }
 }
@@ -1333,7 +1315,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
     const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
     const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
-    float* dbias = reinterpret_cast<float*>(d.bias);
+    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
     float acc[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) acc[j] = 0.f;
@@ -1431,10 +1413,10 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
         for (int q = 0; q < RPI; ++q) v += red[j * 256 + q * FC + ch];
         if (j < 8 * K) {
             const int f = ch * 8 + j / K, k = j % K;
-            if (f < F) atomicAdd(reinterpret_cast<float*>(d.out) + (int64_t)f * K + k, v);
+            if (f < F) fx_add(reinterpret_cast<long long*>(d.out) + (int64_t)f * K + k, v);
         } else {
             const int f = ch * 8 + (j - 8 * K);
-            if (dbias && f < F) atomicAdd(dbias + f, v);
+            if (dbias && f < F) fx_add(dbias + f, v);
         }
     }
 }
@@ -1540,7 +1522,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
             }
         }
         __syncthreads();
-        float* ws = reinterpret_cast<float*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 2 * N;   // stripe
+        long long* ws = reinterpret_cast<long long*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 4 * N;   // stripe
         for (int c = t; c < N; c += 256) {
             float a = 0.f, b = 0.f;
             for (int g = 0; g < G; ++g)
@@ -1549,8 +1531,8 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
                     a += red[g * 8 * N + c + m * N];
                     b += red[2048 + g * 8 * N + c + m * N];
                 }
-            atomicAdd(ws + c, a);
-            atomicAdd(ws + N + c, b);
+            fxw_add(ws + 2 * c, a);
+            fxw_add(ws + 2 * (N + c), b);
         }
     }
 }
@@ -1569,7 +1551,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
     const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
     const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
-    float* dbias = reinterpret_cast<float*>(d.bias);
+    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
     int ro[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) ro[j] = (8 * i + j) / F;
@@ -1639,8 +1621,8 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int m = 0; m < 8; ++m) v += red[p * 2048 + g * 8 * F + c + m * F];
-        if (p < K) atomicAdd(reinterpret_cast<float*>(d.out) + (int64_t)c * K + p, v);
-        else if (dbias) atomicAdd(dbias + c, v);
+        if (p < K) fx_add(reinterpret_cast<long long*>(d.out) + (int64_t)c * K + p, v);
+        else if (dbias) fx_add(dbias + c, v);
     }
 }
 
@@ -1821,30 +1803,24 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     }
     if (flags & GF_OUT_F32) {
         float* o = reinterpret_cast<float*>(d.out);
-        const bool split = (MODE == MODE_FWD) && (flags & GF_SPLITK);   // linear activation only
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
             const int col = n0 + wc * (BN / 2) + j * 16 + r16;
             if (col >= N) continue;
-            const float bv = (bias && (!split || kt0 == 0)) ? bias[col] : 0.f;
+            const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = m0 + wr * 64 + i * 16 + rq + r;
                     if (row >= M) continue;
-                    if (split) atomicAdd(o + (int64_t)row * N + col, acc[i][j][r] + bv);
-                    else o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
+                    o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
                 }
         }
         return;
     }
     bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
     const bool accum = (flags & GF_ACCUM) != 0;
-    // GF_EPI_DACT: the output is the producer's dZ = dX * act'(Y) (single writer: never with accum)
-    const bool edact = MODE == MODE_DGRAD && (flags & GF_EPI_DACT) != 0;
-    const bf16_t* __restrict__ ye = reinterpret_cast<const bf16_t*>(d.bias);
-    const int eact = (flags >> 10) & 3;
     if (n0 == 0 && N <= BN) {
         // the block's rows [m0, m0 + nrows) x all N columns are one contiguous range of the output
         bf16_t* st = lds;                            // k loop done (last barrier above)
@@ -1872,18 +1848,11 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 #pragma unroll
                 for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(p.h[e]));
             }
-            if (edact) {
-                Frag yv;
-                yv.u = *reinterpret_cast<const uint4*>(&ye[(int64_t)m0 * N + v * 8]);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) f.h[e] = f2bf(bf2f(f.h[e]) * act_grad_from_y(bf2f(yv.h[e]), eact));
-            }
             *reinterpret_cast<uint4*>(&dst[v * 8]) = f.u;
         }
         for (int e = nvec * 8 + t; e < total; e += 256) {
             float v = bf2f(st[e]);
             if (accum) v += bf2f(dst[e]);
-            if (edact) v = bf2f(f2bf(v)) * act_grad_from_y(bf2f(ye[(int64_t)m0 * N + e]), eact);
             dst[e] = f2bf(v);
         }
         return;
@@ -1919,11 +1888,6 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
                 for (int e = 0; e < 8; ++e)
                     if (e < nv) f.h[e] = f2bf(bf2f(f.h[e]) + bf2f(o[g + e]));
             }
-            if (edact) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (e < nv) f.h[e] = f2bf(bf2f(f.h[e]) * act_grad_from_y(bf2f(ye[g + e]), eact));
-            }
             if (nv == 8 && (g & 7) == 0) {
                 *reinterpret_cast<uint4*>(o + g) = f.u;
             } else if (nv == 8 && (g & 3) == 0) {
@@ -1948,7 +1912,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 //                 FWD LDS-halo convolution: 2000 + NT (1, 2, 4) + 10 * RT (1, 2, 4) + 100 * patch tier
 //                 (0: 16 KB, 1: 32 KB, 2: 64 KB);
 //                 tiles (prob, b, m0, ntile)
-// variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64, 128, 160}, BNK in {64, 128, 256}
+// variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {16, 64, 128, 256}
 //                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, + 200: super-row form; F % 8 != 0);
 //                 tiles (prob, row block, 0, 0)
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
@@ -1995,19 +1959,10 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
-        W3(128, 128) W3(160, 128) W3(128, 64) W3(160, 64) W3(96, 64)
-#define W8(BMF_, BNK_) \
-    if (v == BMF_ * 1000 + BNK_ + 500) { \
-        const dim3 b8(512); \
-        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true, 8>), grid, b8, 0, s, dp, tp); \
-        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 8>), grid, b8, 0, s, dp, tp); \
-        SERANN_CHECK(hipGetLastError()); return; }
-        W8(128, 128) W8(160, 128) W8(128, 64) W8(160, 64) W8(192, 64)
-#undef W8
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
     }
-    if ((mode == MODE_FWD || mode == MODE_DGRAD) && variant >= 2000 && variant < 3000) {   // DGRAD: GF_VPAD rows
+    if (mode == MODE_FWD && variant >= 2000 && variant < 3000) {
         const int v = variant - 2000;
 #define C3T(NT_, RT_, TIER_, PATCH_)                                                                  \
     if (v == 100 * TIER_ + NT_ + 10 * RT_) {                                                          \

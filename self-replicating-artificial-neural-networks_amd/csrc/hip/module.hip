@@ -10,12 +10,11 @@ namespace py = pybind11;
 static py::dict desc_sizes() {
     py::dict d;
     d["GemmDesc"] = sizeof(GemmDesc);
-    d["ActBwdDesc"] = sizeof(ActBwdDesc);
     d["BnDesc"] = sizeof(BnDesc);
     d["PoolDesc"] = sizeof(PoolDesc);
     d["CopyDesc"] = sizeof(CopyDesc);
     d["LossDesc"] = sizeof(LossDesc);
-    d["TransDesc"] = 5 * sizeof(int64_t);
+    d["TransDesc"] = sizeof(TransDesc);
     d["ImcolDesc"] = sizeof(ImcolDesc);
     d["SplitFinDesc"] = sizeof(SplitFinDesc);
     d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
@@ -26,10 +25,6 @@ static py::dict desc_sizes() {
 PYBIND11_MODULE(serann_hip, m) {
     m.doc() = "SeRANN-AMD HIP/CDNA4 kernels (gfx950)";
     m.def("desc_sizes", &desc_sizes);
-    m.def("grouped_gemm", &launch_grouped_gemm, py::arg("mode"), py::arg("descs"), py::arg("tiles"),
-          py::arg("ntiles"), py::arg("stream"));
-    m.def("gemm2", &launch_gemm2, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
-          py::arg("ntiles"), py::arg("stream"));
     m.def("gemm3", &launch_gemm3, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
           py::arg("ntiles"), py::arg("stream"));
     m.def("transpose_weights", &launch_transpose_weights);
@@ -37,7 +32,6 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("f32_to_bf16", &launch_f32_to_bf16);
     m.def("gather_batch", &launch_gather_batch);
     m.def("counter_add", &launch_counter_add);
-    m.def("act_bwd", &launch_act_bwd);
     m.def("bn", &launch_bn);
     m.def("pool", &launch_pool);
     m.def("convpool", &launch_convpool);

@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 // ---- descriptor layouts (all fields int64 so Python can build them as int64 arrays) ----------
-// Grouped implicit-GEMM convolution problem (see gemm.hip for the per-mode meaning of a/b/out).
+// Grouped implicit-GEMM convolution problem (see gemm3.hip for the per-mode meaning of a/b/out).
 struct GemmDesc {
     int64_t a, b, out, bias, aux;     // aux: DGRAD/FWD accumulate source (unused = 0)
     int64_t H, W, C, OH, OW, F, KH, KW, SH, SW;
@@ -24,25 +24,15 @@ enum GemmFlags : int64_t {
     GF_VEC_B = 2,         // B operand chunks are contiguous 8-element vectors
     GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
     GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
-    GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores instead of fp32 atomics
+    GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores of the Q32 gradient instead of atomics
     GF_SPLITWS = 64,      // FWD (LDS-tiled kernel): k range split over blocks; each split stores its raw
                           // fp32 partial tile to the workspace aux[split][M][N]; splitk_finalize sums
-                          // the splits and applies bias + activation (no atomics, no zeroing)
+                          // the splits in order and applies bias + activation (no atomics, no zeroing)
     GF_BNSTAT = 128,      // FWD narrow kernel: also accumulate the consuming BatchNorm's phase-0 statistics
-                          // into aux (shifted sums, aux[c] and aux[N + c])
-    GF_VPAD = 256,        // FWD halo conv kernel: the input is dZ of a stride-1 conv, virtually zero-padded by
-                          // (KH-1, KW-1) on every side (H, W are the padded extents) and the weights are the
-                          // transposed Wt[C][KH][KW][F] read with flipped taps: a DGRAD computed as a FWD conv
-    GF_EPI_DACT = 512,    // DGRAD (LDS-tiled kernel): out = result * act'(Y), Y = bf16 [M][N] at desc.bias, act code in
-                          // flags bits 10-11 -- the consumer writes its producer's dZ (a concat K slice whose
-                          // producing Dense has no other consumer)
-    GF_SPLITK = 32,       // FWD (LDS-tiled kernel, fp32 output): k range split over blocks; fp32 atomics
-                          // into a zeroed output, the bias added by the split that starts at k = 0
+                          // into aux (shifted sums, wide fixed point: the BN statistics workspace format)
 };
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
-void launch_grouped_gemm(int mode, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
-void launch_gemm2(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 
@@ -56,7 +46,6 @@ void launch_gather_batch(uint64_t x_all, uint64_t g_all, uint64_t y_all, uint64_
                          int64_t base, int64_t B, int64_t n_perm, int64_t x_cols, int64_t g_cols,
                          uint64_t x_out, uint64_t g_out, uint64_t y_out, uint64_t stream);
 void launch_counter_add(uint64_t counter, int64_t value, uint64_t stream);
-void launch_act_bwd(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_bn(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_pool(int backward, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
@@ -77,9 +66,10 @@ void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t 
 void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);
 
 // ---- auxiliary descriptors (int64 fields) ----------------------------------------------------
-struct ActBwdDesc { int64_t dy, y, dz, dbias, M, N, act, flags; };          // flags: 1 = write dz
-// BatchNorm statistics workspace: BN_WS_STRIPES copies of [2][C] fp32 sums (C <= 256 problems), one
-// per block-index residue, summed by the readers (aux.hip wsum)
+struct TransDesc { int64_t src, dst, F, P, C; };                             // P = KH*KW
+// BatchNorm statistics workspace: BN_WS_STRIPES copies of the [2C] sums, each a wide fixed-point pair
+// (hi, lo) of int64 (common.h fxw_add), one copy per block-index residue (same-address atomics serialise
+// in L2), summed in integer arithmetic by the readers (common.h fxw_sum): [stripe][2C][2] int64
 constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;

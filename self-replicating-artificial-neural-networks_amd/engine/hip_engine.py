@@ -37,10 +37,7 @@ import os
 
 ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp32
 SLACK = 64  # elements of zeroed tail on every arena
-# v3 (default): buffer-load direct-fragment FWD/DGRAD with magic-number im2col + 64-row WGRAD;
-# v2: first direct-fragment version; v1: LDS-tiled version.  Kept selectable for A/B measurements.
 FUSE_BN_STATS = os.environ.get("SERANN_FUSE_BN_STATS", "1") != "0"
-GEMM_IMPL = os.environ.get("SERANN_GEMM", "v3")
 FUSE_CONVPOOL = os.environ.get("SERANN_FUSE_CONVPOOL", "1") != "0"
 FUSE_GCHAIN = os.environ.get("SERANN_FUSE_GCHAIN", "1") != "0"
 
@@ -49,7 +46,7 @@ def convpool_pairs(ir: OrganismIR) -> Dict[int, int]:
     """Conv2D nodes on the raw single-channel image whose only consumer is a MaxPool2D: conv id -> pool
     id.  Such a pair runs as one fused kernel (csrc/hip/convpool.hip) and the conv output -- and its
     gradient -- is never materialised (SERANN_FUSE_CONVPOOL=0 turns it off)."""
-    if not FUSE_CONVPOOL or GEMM_IMPL != "v3":
+    if not FUSE_CONVPOOL:
         return {}
     consumers: Dict[int, List[int]] = {}
     for n in ir.nodes:
@@ -69,7 +66,7 @@ def convpool_pairs(ir: OrganismIR) -> Dict[int, int]:
         pa = ir.node(cons[0]).attrs
         if pa["c"] != a["f"] or pa["h"] != a["oh"] or pa["w"] != a["ow"]:
             continue
-        if not H.convpool_ok(a["h"], a["w"], a["kh"], a["kw"]):
+        if not H.convpool_ok(a["h"], a["w"], a["kh"], a["kw"], pa["ph"], pa["pw"]):
             continue
         out[n.id] = cons[0]
     return out
@@ -83,7 +80,7 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
     (<= 16 taps and a gchain_variant for the filter / unit counts); the BatchNormalization joins when it
     is the Dense's only consumer and normalises its last axis.  The conv output -- and, with the BN, the
     Dense output -- and their gradients are never materialised (SERANN_FUSE_GCHAIN=0 turns it off)."""
-    if not FUSE_GCHAIN or GEMM_IMPL != "v3":
+    if not FUSE_GCHAIN:
         return {}
     consumers: Dict[int, List[int]] = {}
     for n in ir.nodes:
@@ -105,7 +102,7 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
             continue
         da = dn.attrs
         if (da["cin"] != a["f"] or da["h"] != a["oh"] or da["w"] != 1 or da["act"] not in H.ACT_CODES
-                or H.gchain_variant(a["f"], da["f"], a["kh"]) is None):
+                or H.gchain_variant(a["f"], da["f"], a["kh"]) is None or not H.gchain_fits(a["oh"], a["h"])):
             continue
         bn = None
         dc = consumers.get(dn.id, [])
@@ -214,18 +211,12 @@ class Plan:
         s = H.stream_handle()
         for la in self.launches:
             k = la.kind
-            if k == "gemm":
-                L.grouped_gemm(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
-            elif k == "gemm3":
+            if k == "gemm3":
                 L.gemm3(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
-            elif k == "gemm2":
-                L.gemm2(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "transpose":
                 L.transpose_weights(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "imcol":
                 L.imcol(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
-            elif k == "act_bwd":
-                L.act_bwd(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "bn":
                 L.bn(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "pool":
@@ -307,7 +298,8 @@ class HipPopulationEngine(PopulationEngine):
             self.wt_off.append(d)
         self.wt = torch.zeros(max(wt_size, ALIGN) + SLACK, dtype=torch.bfloat16, device=dev)
         self.p = self.parena.materialize()
-        self.g = torch.zeros_like(self.p)
+        # gradients: deterministic Q32 fixed-point accumulator (csrc/hip/common.h fx_*), converted by Adam
+        self.g = torch.zeros(self.p.numel(), dtype=torch.int64, device=dev)
         self.m = torch.zeros_like(self.p)
         self.v = torch.zeros_like(self.p)
         self.pbf = torch.zeros(self.p.numel() + SLACK, dtype=torch.bfloat16, device=dev)
@@ -463,13 +455,14 @@ class HipPopulationEngine(PopulationEngine):
                         rec["grad"][n.id] = grad.alloc(B * math.prod(n.shape))
                 rec["req"] = req
             bufs.append(rec)
-        # BN workspaces contiguous so one memset zeroes them all
-        ws = Arena(torch.float32, dev)
+        # BN statistics workspaces (wide fixed point: [stripe][2C][hi, lo] int64, csrc/hip/common.h fxw_*),
+        # contiguous so one memset zeroes them all
+        ws = Arena(torch.int64, dev)
         for lay, rec in zip(self.layouts, bufs):
             for nid, d in rec["bn"].items():
                 c = lay.ir.node(nid).attrs["channels"]
-                d["ws"] = ws.alloc(2 * c * H.BN_WS_STRIPES)
-                d["wsb"] = ws.alloc(2 * c * H.BN_WS_STRIPES)
+                d["ws"] = ws.alloc(H.bn_ws_words(c))
+                d["wsb"] = ws.alloc(H.bn_ws_words(c))
         act.materialize(zero=True)
         grad.materialize(zero=True)
         f32.materialize(zero=True)
@@ -521,7 +514,7 @@ class HipPopulationEngine(PopulationEngine):
         P = self.num_organisms
         fcat = [dict() for _ in range(P)]
         fcons = [dict() for _ in range(P)]
-        if os.environ.get("SERANN_FUSE_CONCAT", "1") == "0" or GEMM_IMPL != "v3":
+        if os.environ.get("SERANN_FUSE_CONCAT", "1") == "0":
             return fcat, fcons
         for o, lay in org_iter():
             ir = lay.ir
@@ -618,53 +611,29 @@ class HipPopulationEngine(PopulationEngine):
             if not rows:
                 return
             assert len(rows) == len(dims), (len(rows), len(dims))
-            if GEMM_IMPL == "v1":
-                if mode_ == H.MODE_DGRAD:
-                    rows = [dict(r, b=r["b_v1"]) for r in rows]
-                rows = [{k: v for k, v in r.items() if k != "b_v1"} for r in rows]
-                tiles = H.gemm_tiles(dims, mode_)
-                if len(tiles):
-                    plan.launches.append(Launch("gemm", mode_, desc_tensor(rows, H.GEMM_DTYPE), T(tiles), len(tiles)))
-                return
-            if GEMM_IMPL == "v3":
-                clean = [{k: val for k, val in r.items() if k != "b_v1"} for r in rows]
-                for v, rws, tiles in H.gemm3_plan(mode_, clean, dims, splitk=True):
-                    if not len(tiles):
-                        continue
-                    # split-K FWD problems (merged Dense): fp32 partials per split in a workspace of
-                    # the plan, then one grouped finalize launch (sum of splits + bias + activation)
-                    fin = []
-                    for r in rws:
-                        ns = int(r.pop("_split", 1))
-                        if ns > 1 and not r.get("_pre"):
-                            wsb = torch.zeros(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
-                            plan.keep.append(wsb)
-                            r["aux"] = wsb.data_ptr()
-                            fin.append(dict(ws=r["aux"], out=r["out"], bias=r.get("bias", 0), M=r["M"], N=r["N"],
-                                            S=ns, act=r.get("act", 0)))
-                    plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
-                                                len(tiles)))
-                    if fin:
-                        add_chunked("splitfin", 0, fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in fin],
-                                    H.SPLITFIN_ELEMS)
-                if extra_fin:
-                    # K slices of fused-concat consumers (every variant launched above): one finalize
-                    add_chunked("splitfin", 0, extra_fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in extra_fin],
+            for v, rws, tiles in H.gemm3_plan(mode_, rows, dims, splitk=True):
+                if not len(tiles):
+                    continue
+                # split-K FWD problems (merged Dense): fp32 partials per split in a workspace of
+                # the plan, then one grouped finalize launch (ordered sum of splits + bias + activation)
+                fin = []
+                for r in rws:
+                    ns = int(r.pop("_split", 1))
+                    if ns > 1 and not r.get("_pre"):
+                        wsb = torch.zeros(ns * int(r["M"]) * int(r["N"]), dtype=torch.float32, device=self.device)
+                        plan.keep.append(wsb)
+                        r["aux"] = wsb.data_ptr()
+                        fin.append(dict(ws=r["aux"], out=r["out"], bias=r.get("bias", 0), M=r["M"], N=r["N"],
+                                        S=ns, act=r.get("act", 0)))
+                plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
+                                            len(tiles)))
+                if fin:
+                    add_chunked("splitfin", 0, fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in fin],
                                 H.SPLITFIN_ELEMS)
-                return
-            groups = {}
-            for r, dm in zip(rows, dims):
-                v = H.gemm2_variant(mode_, dm[0], dm[1], dm[2])
-                groups.setdefault(v, ([], []))
-                groups[v][0].append({k: val for k, val in r.items() if k != "b_v1"})
-                groups[v][1].append(dm)
-            for v in sorted(groups):
-                rws, dms = groups[v]
-                bm, bn = H.gemm2_block(mode_, v)
-                tiles = H.gemm_tiles(dms, mode_, bm=bm, bn=bn)
-                if len(tiles):
-                    plan.launches.append(Launch("gemm2", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
-                                                len(tiles)))
+            if extra_fin:
+                # K slices of fused-concat consumers (every variant launched above): one finalize
+                add_chunked("splitfin", 0, extra_fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in extra_fin],
+                            H.SPLITFIN_ELEMS)
 
         def add_chunked(kind, arg, rows, dtype, counts, chunk):
             if not rows:
@@ -683,7 +652,7 @@ class HipPopulationEngine(PopulationEngine):
             return self.p.data_ptr() + off * 4
 
         def gptr(off):
-            return self.g.data_ptr() + off * 4
+            return self.g.data_ptr() + off * 8          # Q32 int64 gradient arena
 
         def sptr(off):
             return self.stats.data_ptr() + off * 4
@@ -691,9 +660,9 @@ class HipPopulationEngine(PopulationEngine):
         f32a = mem["f32"]
 
         # Shared im2col of the raw inputs: when every organism reads the same input batch, all
-        # first-layer convolutions with the same (KH, KW, SH, SW) share one materialised im2col
-        # matrix, and their FWD / WGRAD become aligned 1x1 problems (v2 only).
-        shared_inputs = GEMM_IMPL != "v1" and all(inp == inputs[0] for inp in inputs)
+        # first-layer convolutions with the same (KH, KW, SH, SW) that are not fused with their pool
+        # share one materialised im2col matrix, and their FWD / WGRAD become aligned 1x1 problems.
+        shared_inputs = all(inp == inputs[0] for inp in inputs)
         imcol: Dict[tuple, dict] = {}
 
         def raw_conv_imcol(o, n):
@@ -746,11 +715,10 @@ class HipPopulationEngine(PopulationEngine):
                 by_kt.setdefault(r.pop("_kt"), []).append(r)
             for kt in sorted(by_kt):
                 rws = by_kt[kt]
-                imgs = H.convpool_wgrad_imgs([(r["B"], r["F"]) for r in rws]) if backward else 0
                 for r in rws:
-                    r["flags"] = imgs
+                    r["flags"] = H.convpool_wgrad_imgs(r["B"], r["F"]) if backward else 0
                 add_chunked("convpool", (1 if backward else 0, kt), rws, H.CONVPOOL_DTYPE,
-                            [H.convpool_chunks(r["B"], r["F"], backward, imgs) for r in rws], 1)
+                            [H.convpool_chunks(r["B"], r["F"], backward, r["flags"]) for r in rws], 1)
         def gchain_row(o, last):
             """Descriptor of the fused genotype chain ending at node ``last`` of organism ``o``."""
             lay_ = self.layouts[o]
@@ -795,7 +763,7 @@ class HipPopulationEngine(PopulationEngine):
                 counts = []
                 for r in rws:
                     R_ = int(r["B"]) * int(r["L1"])
-                    r["rpb"] = H.gchain_rpb(R_, len(rws), mode_, int(r["L1"]), int(r["L0"]))
+                    r["rpb"] = H.gchain_rpb(R_, mode_, int(r["L1"]), int(r["L0"]))
                     counts.append(-(-R_ // r["rpb"]))
                 tiles = H.chunk_tiles(counts, 1)
                 if len(tiles):
@@ -978,7 +946,7 @@ class HipPopulationEngine(PopulationEngine):
                 NC, L = ir.num_classes, ir.genotype_size
                 rows.append(dict(logits=self._act_ptr(mem, o, ir.cls_head, inputs),
                                  dlogits=mem["grad"].ptr(rec["grad"][ir.cls_head]) if train else 0,
-                                 labels=label_ptr, target=target_ptrs[o], metrics=metrics.data_ptr() + 16 * o,
+                                 labels=label_ptr, target=target_ptrs[o], metrics=metrics.data_ptr() + 32 * o,
                                  NC=NC, L=L, B=B, lb=self.lb[o]))
             plan.loss = (desc_tensor(rows, H.LOSS_DTYPE), len(rows), B)
         else:
@@ -1002,30 +970,29 @@ class HipPopulationEngine(PopulationEngine):
                 return None
             return own
 
-        if GEMM_IMPL != "v1":
-            trows, tcnt = [], []
-            for o, lay in org_iter():
-                ir = lay.ir
-                for nid, off in lay.w.items():
-                    a = ir.node(nid).attrs
-                    if nid in mem["orgs"][o]["gc_nodes"]:
-                        continue                      # fused genotype chain: no DGRAD launch
-                    if a["kind"] == "head_cls":
-                        F_, P_, C_ = ir.num_classes + ir.genotype_size, 1, ir.head_features
-                    else:
-                        F_, P_, C_ = a["f"], a["kh"] * a["kw"], a["cin"]
-                    # the transposed copy Wt[C][KH][KW][F] only feeds DGRAD kernels that cannot read the
-                    # natural layout, and only layers whose input needs a gradient have a DGRAD at all
-                    if nid in fcons[o]:
-                        needs_dgrad = any(target(o, pid) is not None for pid, _, _ in fcat[o][fcons[o][nid]])
-                    else:
-                        needs_dgrad = target(o, ir.node(nid).inputs[0]) is not None
-                    if not needs_dgrad or H.dgrad_reads_natural(a["kh"], a["kw"], a["sh"], a["sw"], F_):
-                        continue
-                    trows.append(dict(src=wptr_bf(off), dst=self.wt.data_ptr() + 2 * self.wt_off[o][nid], F=F_, P=P_,
-                                      C=C_))
-                    tcnt.append(-(-(F_ * P_ * C_) // H.TRANS_ELEMS))
-            add_chunked("transpose", 0, trows, H.TRANS_DTYPE, tcnt, 1)
+        trows, tcnt = [], []
+        for o, lay in org_iter():
+            ir = lay.ir
+            for nid, off in lay.w.items():
+                a = ir.node(nid).attrs
+                if nid in mem["orgs"][o]["gc_nodes"]:
+                    continue                      # fused genotype chain: no DGRAD launch
+                if a["kind"] == "head_cls":
+                    F_, P_, C_ = ir.num_classes + ir.genotype_size, 1, ir.head_features
+                else:
+                    F_, P_, C_ = a["f"], a["kh"] * a["kw"], a["cin"]
+                # the transposed copy Wt[C][KH][KW][F] only feeds DGRAD kernels that cannot read the
+                # natural layout, and only layers whose input needs a gradient have a DGRAD at all
+                if nid in fcons[o]:
+                    needs_dgrad = any(target(o, pid) is not None for pid, _, _ in fcat[o][fcons[o][nid]])
+                else:
+                    needs_dgrad = target(o, ir.node(nid).inputs[0]) is not None
+                if not needs_dgrad or H.dgrad_reads_natural(a["kh"], a["kw"], a["sh"], a["sw"], F_):
+                    continue
+                trows.append(dict(src=wptr_bf(off), dst=self.wt.data_ptr() + 2 * self.wt_off[o][nid], F=F_, P=P_,
+                                  C=C_))
+                tcnt.append(-(-(F_ * P_ * C_) // H.TRANS_ELEMS))
+        add_chunked("transpose", 0, trows, H.TRANS_DTYPE, tcnt, 1)
 
         # BatchNormalization whose input is the output of an activated GEMM used by nothing else: its
         # backward (phase 5) writes that GEMM's dZ = dx * act'(x) directly, so the GEMM's WGRAD / DGRAD
@@ -1051,45 +1018,8 @@ class HipPopulationEngine(PopulationEngine):
                             and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
                         dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
 
-        # A Dense (relu / sigmoid) whose only consumer is a fused concat read by a single GEMM: that
-        # GEMM's K-slice DGRAD (LDS-tiled kernel) writes the Dense's dZ = dX * act'(Y) in its epilogue
-        # (GF_EPI_DACT), so the Dense's WGRAD / DGRAD read dZ alone instead of dY and Y
-        # Opt-in (SERANN_FOLD_CONCAT_ACT=1): measured neutral on population B (step 19.85 vs 19.93 ms; the
-        # slice DGRAD's extra Y read cost what the producer's WGRAD / DGRAD saved; profiles/r2e/ab_concat_act_fold.txt)
-        epi_fold = [dict() for _ in range(P)]          # concat input id -> act code
-        if os.environ.get("SERANN_FOLD_CONCAT_ACT", "0") == "1" and "tiled" not in H._OFF:
-            for o, lay in org_iter():
-                ir = lay.ir
-                rec = mem["orgs"][o]
-                owner = rec["owner"]
-                uses: Dict[int, int] = {}
-                for n in ir.nodes:
-                    if n.op == "reshape":
-                        continue
-                    for i in n.inputs:
-                        uses[owner.get(i, i)] = uses.get(owner.get(i, i), 0) + 1
-                for cid, parts in fcat[o].items():
-                    cons = [g for g, c in fcons[o].items() if c == cid]
-                    if len(cons) != 1:
-                        continue
-                    cn = ir.node(cons[0])
-                    fc = ir.num_classes + ir.genotype_size if cn.attrs["kind"] == "head_cls" else cn.attrs["f"]
-                    if fc <= H.BK:
-                        continue                  # the slice DGRAD would not run on the LDS-tiled kernel
-                    for pid, _, _ in parts:
-                        src = ir.node(owner.get(pid, pid))
-                        if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
-                                and src.id not in rec["fused_convs"] and src.id not in rec["gc_nodes"]
-                                and src.attrs["act"] in ("relu", "sigmoid") and uses.get(src.id, 0) == 1
-                                and rec["req"].get(src.id, False) and src.id not in dz_folded[o]
-                                and target(o, pid) == src.id):
-                            dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
-                            epi_fold[o][pid] = H.ACT_CODES[src.attrs["act"]]
-        self.concat_act_folds = sum(len(f) for f in epi_fold)     # (introspection: tests)
-
         STAGES = ("dgrad", "pool", "bn", "copy")
         for d in range(maxd, 0, -1):
-            ab_rows, ab_cnt = [], []
             wg_rows, wg_dims = [], []
             bn_red, bn_red_cnt = [], []
             cpw_rows = []
@@ -1133,15 +1063,10 @@ class HipPopulationEngine(PopulationEngine):
                         M = B * OH * OW
                         K = KH * KW * C
                         dbias = gptr(lay.b[n.id]) if n.id in lay.b else 0
-                        fused = GEMM_IMPL != "v1"
-                        if not fused and (act != 0 or dbias):
-                            ab_rows.append(dict(dy=dz, y=yv, dz=dz, dbias=dbias, M=M, N=F, act=act,
-                                                flags=1 if act != 0 else 0))
-                            ab_cnt.append(H.red_chunks(M, F))
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-                        ic = raw_conv_imcol(o, n) if fused and not head else None
-                        if fused and n.id in fcons[o]:
+                        ic = raw_conv_imcol(o, n) if not head else None
+                        if n.id in fcons[o]:
                             # fused-concat consumer: WGRAD and DGRAD per K slice, in place on the concat
                             # inputs and their gradient buffers (no concat copy, no DGRAD for inputs
                             # without a gradient, e.g. the raw image)
@@ -1155,42 +1080,29 @@ class HipPopulationEngine(PopulationEngine):
                                 wg_dims.append((F, width, M))
                                 own_p = target(o, pid)
                                 if own_p is not None:
-                                    base = dict(a=dz, b=self.wt.data_ptr() + 2 * (self.wt_off[o][n.id] + col * F), b_v1=0,
+                                    base = dict(a=dz, b=self.wt.data_ptr() + 2 * (self.wt_off[o][n.id] + col * F),
                                                 _bnat=wptr_bf(lay.w[n.id]) + 2 * col, _bnat_ld=D,
                                                 aux=yv, act=act, out=mem["grad"].ptr(rec["grad"][own_p]), H=Hh, W=1,
                                                 C=width, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=width, K=F)
-                                    efl = 0
-                                    if pid in epi_fold[o]:
-                                        base["bias"] = self._act_ptr(mem, o, pid, inputs)   # the producer's Y
-                                        efl = H.GF_EPI_DACT | (epi_fold[o][pid] << 10)
-
-                                    def mk(acc, r=base, e=efl):
-                                        if acc and e:
-                                            raise RuntimeError("GF_EPI_DACT slice is not the only gradient writer")
-                                        return dict(r, flags=(H.GF_ACCUM if acc else 0) | e)
-                                    tasks["dgrad"].append((o, own_p, mk, (M, width, F)))
+                                    tasks["dgrad"].append((o, own_p, lambda acc, r=base: dict(r, flags=H.GF_ACCUM if acc else 0),
+                                                           (M, width, F)))
                             continue
                         if ic is not None:
                             wg_rows.append(dict(a=dz, b=ic["buf"].data_ptr(), out=gptr(lay.w[n.id]), bias=dbias,
                                                 aux=yv, act=act, H=OH, W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1,
                                                 SH=1, SW=1, M=F, N=K, K=M, flags=vec))
                             wg_dims.append((F, K, M))
-                        elif fused:
-                            # v2: dZ = dY * act'(Y) on load; the bias gradient is reduced inside WGRAD
+                        else:
+                            # dZ = dY * act'(Y) on load; the bias gradient is reduced inside WGRAD
                             wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), bias=dbias, aux=yv, act=act,
                                                 H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW,
                                                 M=F, N=K, K=M, flags=vec))
                             wg_dims.append((F, K, M))
-                        else:
-                            wg_rows.append(dict(a=dz, b=xin, out=gptr(lay.w[n.id]), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F,
-                                                KH=KH, KW=KW, SH=SH, SW=SW, M=F, N=K, K=M, flags=vec))
-                            wg_dims.append((F, K, M))
                         own = target(o, n.inputs[0])
                         if own is not None:
                             Mi = B * Hh * Ww
-                            base = dict(a=dz, b=self.wt.data_ptr() + 2 * self.wt_off[o][n.id], b_v1=wptr_bf(lay.w[n.id]),
-                                        _bnat=wptr_bf(lay.w[n.id]),
-                                        aux=yv if fused else 0, act=act if fused else 0,
+                            base = dict(a=dz, b=self.wt.data_ptr() + 2 * self.wt_off[o][n.id],
+                                        _bnat=wptr_bf(lay.w[n.id]), aux=yv, act=act,
                                         out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
                                         W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,
                                         K=KH * KW * F)
@@ -1248,7 +1160,6 @@ class HipPopulationEngine(PopulationEngine):
                             col += inner
                     else:
                         fb.append((o, n))
-            add_chunked("act_bwd", 0, ab_rows, H.ACTBWD_DTYPE, ab_cnt, 1)
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             add_convpool(cpw_rows, True)
             add_gchain([r for r in gcb_rows if r["_bn"]], H.GC_BSTAT)
@@ -1407,7 +1318,7 @@ class HipPopulationEngine(PopulationEngine):
                         gg = grads[k]
                         k += 1
                         if gg is not None:
-                            self.g.narrow(0, d[n.id], c).add_(gg)
+                            self.g.narrow(0, d[n.id], c).add_(H.to_q32(gg))
         return fn
 
     def _fallback_compute_params(self, o, n, xs, params):
@@ -1458,7 +1369,7 @@ class HipPopulationEngine(PopulationEngine):
         self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
         perm_t = torch.zeros(max(split, 1), dtype=torch.int32, device=dev)
         counter = torch.zeros(1, dtype=torch.int32, device=dev)
-        metrics = torch.zeros(P, 4, dtype=torch.float32, device=dev)
+        metrics = torch.zeros(P, 4, dtype=torch.int64, device=dev)      # Q32 fixed point (aux.hip loss_kernel)
 
         t_plan = time.perf_counter()
         mem = self._alloc_buffers(B, with_grads=True)
@@ -1503,7 +1414,7 @@ class HipPopulationEngine(PopulationEngine):
             L.gather_batch(dd["train_x"].data_ptr(), dd["train_g"].data_ptr(), dd["train_y"].data_ptr(),
                            perm_t.data_ptr(), counter.data_ptr() if ctr else 0, base, nb, split, xcols, gcols,
                            xb.data_ptr(), gb.data_ptr(), yb.data_ptr(), s)
-            L.memset32(wsb.data_ptr(), wsb.numel(), s)
+            L.memset32(wsb.data_ptr(), 2 * wsb.numel(), s)          # int64 workspace
             if len(pls) == 1:
                 run_plan(pls[0])
             else:
@@ -1564,7 +1475,7 @@ class HipPopulationEngine(PopulationEngine):
             if rem_plans is not None and steps > nfull:
                 remainder_step()
                 total += 1
-            m = metrics.cpu().numpy()
+            m = H.from_q32(metrics)
             train_acc = m[:, 1] / np.maximum(m[:, 3], 1)
             if cfg.val_every_epoch or epoch == cfg.epochs - 1:
                 val_acc, val_mse = self._evaluate_rows(dd["train_x"], dd["train_g"], dd["train_y"], split, n, cfg)
@@ -1594,13 +1505,13 @@ class HipPopulationEngine(PopulationEngine):
         gb = torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32, device=dev).to(torch.bfloat16)
         yb = torch.as_tensor(y.astype(np.int32), device=dev)
         self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
-        metrics = torch.zeros(self.num_organisms, 4, dtype=torch.float32, device=dev)
+        metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
         mem = self._alloc_buffers(B, with_grads=True)
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
         plan = self._build_plan("train", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * self.num_organisms, metrics)
         s = H.stream_handle()
         self.g.zero_()
-        self.lib.memset32(mem["ws"].t.data_ptr(), mem["ws"].t.numel(), s)
+        self.lib.memset32(mem["ws"].t.data_ptr(), 2 * mem["ws"].t.numel(), s)
         fwd = Plan()
         fwd.launches = plan.launches[:plan.fwd_count]
         fwd.run()
@@ -1608,14 +1519,14 @@ class HipPopulationEngine(PopulationEngine):
         bwd = Plan()
         bwd.launches = plan.launches[plan.fwd_count:]
         bwd.run()
-        grads = self.g.clone()
+        grads = (self.g.double() / 2.0 ** 32).float()
         if apply_adam:
             c = self.cfg
             self.lib.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
                           self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), c.lr, c.beta1, c.beta2, c.eps, s)
         torch.cuda.synchronize(dev)
         self._debug_mem = mem
-        return grads, metrics.cpu().numpy()
+        return grads, H.from_q32(metrics)
 
     def debug_logits(self, mem=None) -> List[np.ndarray]:
         mem = mem or self._debug_mem
@@ -1637,7 +1548,7 @@ class HipPopulationEngine(PopulationEngine):
             xb = _padded_zeros((B, xcols), torch.bfloat16, dev)
             gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
             yb = torch.zeros(B, dtype=torch.int32, device=dev)
-            metrics = torch.zeros(self.num_organisms, 4, dtype=torch.float32, device=dev)
+            metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
             self._input_tensors = getattr(self, "_input_tensors", {})
             self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
             mem = getattr(self, "_train_mem", None)
@@ -1665,7 +1576,7 @@ class HipPopulationEngine(PopulationEngine):
                            G.shape[1], xb.data_ptr(), gb.data_ptr(), yb.data_ptr(), s)
             plan.run()
             self._run_loss(plan, False, min(B, n - base))
-        m = metrics.cpu().numpy()
+        m = H.from_q32(metrics)
         return m[:, 1] / np.maximum(m[:, 3], 1), m[:, 2] / np.maximum(m[:, 3], 1)
 
     def evaluate(self, x, labels, g, cfg: Optional[TrainConfig] = None) -> np.ndarray:

@@ -20,7 +20,6 @@ GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "
                "sbase",     # GF_SPLITWS: first workspace slot
                "ldo"]       # 64-row WGRAD: output row stride (0: N)
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
-ACTBWD_DTYPE = np.dtype([(f, _I) for f in ["dy", "y", "dz", "dbias", "M", "N", "act", "flags"]])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
                                        "dgamma", "dbeta", "R", "C", "flags"]] + [("eps", np.float64),
                                                                                 ("momentum", np.float64)])
@@ -42,14 +41,12 @@ GC_FSTAT, GC_FAPPLY, GC_BSTAT, GC_BFULL = 0, 1, 2, 3     # gchain.hip modes
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
-GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITK, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 32, 64, 128
-GF_VPAD = 256
-GF_EPI_DACT = 512        # DGRAD on the LDS-tiled kernel: output * act'(Y at desc.bias), act code in flags bits 10-11
+GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 64, 128
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
 BM, BN, BK = 64, 64, 32
-RED_ELEMS = 16384      # aux.hip: elements per block of the channel-strided reductions (BN, act_bwd)
+RED_ELEMS = 16384      # aux.hip: elements per block of the channel-strided reductions (BN with C > 256)
 POOL_ELEMS = 1024
 COPY_ROWS = 16
 
@@ -93,8 +90,28 @@ BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256
 
 
 BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block
-BN_WS_STRIPES = 8      # serann_hip.h: copies of the [2][C] BN statistics workspace (C <= 256)
+BN_WS_STRIPES = 8      # serann_hip.h: copies of the [2C] BN statistics workspace (wide fixed point)
 BN_STAT_SMALL = 2048    # aux.hip: ... unless the problem spans fewer blocks than this at 1x
+
+
+def bn_ws_words(channels: int) -> int:
+    """int64 words of one BatchNorm statistics workspace: BN_WS_STRIPES copies x 2C sums x (hi, lo)
+    (csrc/hip/common.h fxw_add / fxw_sum)."""
+    return BN_WS_STRIPES * 2 * int(channels) * 2
+
+
+Q32 = float(2 ** 32)   # csrc/hip/common.h fx_*: the gradient arena and loss metrics are int64 in 2^-32 units
+
+
+def to_q32(t):
+    """float tensor -> int64 Q32 fixed point (the kernels' fx_q: clamp to +-2^30, round to nearest)."""
+    import torch
+    return torch.round(t.double().clamp(-2.0 ** 30, 2.0 ** 30) * Q32).to(torch.int64)
+
+
+def from_q32(t) -> np.ndarray:
+    """int64 Q32 tensor -> float64 numpy array."""
+    return t.detach().cpu().numpy().astype(np.float64) / Q32
 
 
 def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
@@ -124,16 +141,20 @@ def convpool_variant(kh: int, kw: int, filters: int) -> int:
     return convpool_kt(kh, kw) * 8 + min(4, -(-int(filters) // 16))
 
 
-def convpool_ok(h: int, w: int, kh: int, kw: int) -> bool:
-    """Shapes the fused first-layer Conv2D + MaxPool2D kernels accept (convpool.hip limits)."""
-    return int(h) * int(w) <= CONVPOOL_MAXPIX and 1 <= convpool_kt(kh, kw) <= 3
+def convpool_ok(h: int, w: int, kh: int, kw: int, ph: int = 1, pw: int = 1) -> bool:
+    """Shapes the fused first-layer Conv2D + MaxPool2D kernels accept (convpool.hip limits): the image
+    fits the LDS copy, at most 3 k steps of taps, and at most 256 pool-window offsets (the argmax code
+    is 8 bits, packed into the low mantissa bits of the max key)."""
+    return (int(h) * int(w) <= CONVPOOL_MAXPIX and 1 <= convpool_kt(kh, kw) <= 3
+            and int(ph) * int(pw) <= 256)
 
 
 def gchain_variant(f1: int, f2: int, taps: int):
     """Instantiation (F1K * 8 + F2K) of the fused genotype chain for a Conv1D with ``f1`` filters and
     ``taps`` taps followed by a Dense of ``f2`` units, or None when gchain.hip has none: T <= 16,
     F1 <= 32 with F2 <= 128, or F1 <= 64 with F2 <= 64."""
-    f1k, f2k = -(-int(f1) // 32), -(-int(f2) // 32)
+    f1, f2 = int(f1), int(f2)
+    f1k, f2k = -(-f1 // 32), -(-f2 // 32)
     if not 1 <= int(taps) <= 16 or f1 < 1 or f2 < 1:
         return None
     if (f1k == 1 and f2k <= 4) or (f1k == 2 and f2k <= 2):
@@ -141,22 +162,43 @@ def gchain_variant(f1: int, f2: int, taps: int):
     return None
 
 
-GCHAIN_BLOCKS = {0: 4096, 1: 4096, 2: 8192, 3: 2048}     # target grid size per mode (gchain.hip)
+# target blocks per PROBLEM per mode (gchain.hip; FSTAT, FAPPLY, BSTAT, BFULL).  Per problem, not per
+# launch: a problem's row blocking -- and so the grouping of its fp32 partial sums before they meet in the
+# fixed-point workspaces -- must not depend on which other organisms share the launch, or an organism would
+# train differently in a 2-rank shard than in the whole population (deterministic sharding)
+GCHAIN_BLOCKS = {0: 96, 1: 96, 2: 192, 3: 48}
 GCHAIN_GMAX = 8192                                        # gchain.hip GC_GMAX: staged genotype elements
 
 
-def gchain_rpb(rows: int, nprob: int, mode: int, l1: int = 1, l0: int = 0) -> int:
-    """Rows per block of a fused-chain launch over ``nprob`` problems of ``rows`` rows (conv output
-    length ``l1``, genotype length ``l0``): a multiple of 128 (4 waves x 32-row backward super-tiles)
-    sized so the grid reaches the mode's target block count (the full backward has fewer, longer
-    blocks: one fp32 atomic flush per gradient element and block), and small enough that the block's
-    genotype rows fit the LDS staging buffer."""
-    per = -(-int(rows) * max(1, int(nprob)) // GCHAIN_BLOCKS[int(mode)])
+def gchain_genotype_elems(rpb: int, l1: int, l0: int) -> int:
+    """Upper bound of the genotype elements one fused-chain block stages in LDS (gchain.hip
+    gc_prologue): the rows [R0, R0 + rpb) of the [B * L1] conv output touch at most
+    ceil(rpb / L1) + 1 batch rows of L0 genotype elements."""
+    return (-(-int(rpb) // max(1, int(l1))) + 1) * int(l0)
+
+
+def gchain_fits(l1: int, l0: int) -> bool:
+    """A fused chain is eligible only when a block of the smallest row count (64) stages its genotype
+    rows within GCHAIN_GMAX elements (otherwise the unfused kernels run it)."""
+    return gchain_genotype_elems(64, l1, l0) <= GCHAIN_GMAX
+
+
+def gchain_rpb(rows: int, mode: int, l1: int = 1, l0: int = 0) -> int:
+    """Rows per block of one fused-chain problem of ``rows`` rows (conv output length ``l1``, genotype
+    length ``l0``): a multiple of 64 (128 when the genotype staging allows; 4 waves x 32-row backward
+    super-tiles) sized so the problem gets about GCHAIN_BLOCKS[mode] blocks (the full backward has fewer,
+    longer blocks: one fixed-point atomic flush per gradient element and block), and small enough that the
+    block's genotype rows fit the LDS staging buffer (raises when even 64 rows do not: gchain_fits must
+    have excluded the chain).  A function of the problem alone (deterministic sharding)."""
+    per = -(-int(rows) // GCHAIN_BLOCKS[int(mode)])
     rpb = max(128, -(-per // 128) * 128)
     rpb = min(rpb, -(-int(rows) // 128) * 128)
     if l0 > 0:
-        while rpb > 64 and (-(-rpb // max(1, int(l1))) + 1) * int(l0) > GCHAIN_GMAX:
+        while rpb > 64 and gchain_genotype_elems(rpb, l1, l0) > GCHAIN_GMAX:
             rpb -= 64
+        if gchain_genotype_elems(rpb, l1, l0) > GCHAIN_GMAX:
+            raise ValueError(f"fused genotype chain: {rpb} rows of L1={l1}, L0={l0} exceed the LDS staging "
+                             f"buffer ({GCHAIN_GMAX} elements)")
     return rpb
 
 
@@ -167,12 +209,15 @@ def convpool_chunks(batch: int, filters: int, backward: bool, imgs: int = 0) -> 
     return -(-int(batch) // per) * -(-int(filters) // 64)
 
 
-def convpool_wgrad_imgs(problems) -> int:
-    """Images per block of a grouped fused conv+pool WGRAD launch over (batch, filters) problems:
-    32, halved (down to 8) while the launch has fewer than WGRAD_MIN_BLOCKS blocks."""
+CONVPOOL_MIN_CHUNKS = 16    # fused conv+pool WGRAD: blocks one problem should have at least
+
+
+def convpool_wgrad_imgs(batch: int, filters: int) -> int:
+    """Images per block of one fused conv+pool WGRAD problem: 32, halved (down to 8) while the problem
+    alone has fewer than CONVPOOL_MIN_CHUNKS blocks.  Per problem, so the grouping of the per-wave fp32
+    partial sums does not depend on the other problems of the launch (deterministic sharding)."""
     imgs = CONVPOOL_WGRAD_IMGS
-    while imgs > 8 and "wgrad_minblocks" not in _OFF and \
-            sum(convpool_chunks(b, f, True, imgs) for b, f in problems) < WGRAD_MIN_BLOCKS:
+    while imgs > 8 and convpool_chunks(batch, filters, True, imgs) < CONVPOOL_MIN_CHUNKS:
         imgs //= 2
     return imgs
 
@@ -200,7 +245,7 @@ def available() -> bool:
 
 def check_layouts():
     sizes = lib().desc_sizes()
-    for name, dt in [("GemmDesc", GEMM_DTYPE), ("ActBwdDesc", ACTBWD_DTYPE), ("BnDesc", BN_DTYPE),
+    for name, dt in [("GemmDesc", GEMM_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE)]:
@@ -226,16 +271,6 @@ IMCOL_ROWS = 64
 TRANS_ELEMS = 4096
 
 
-def gemm2_variant(mode: int, M: int, N: int, K: int = 0) -> int:
-    """Tile variant of the v2 kernels: the column tile (FWD/DGRAD) or f tile (WGRAD) in {16, 32, 64};
-    FWD/DGRAD problems with few rows and a long k loop use the wave-split-K form (+1000)."""
-    dim = M if mode == MODE_WGRAD else N
-    v = 16 if dim <= 16 else (32 if dim <= 32 else 64)
-    if mode != MODE_WGRAD and M <= 8192 and -(-K // BK) >= 16:
-        v += 1000
-    return v
-
-
 def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     """Kernel instantiation of the v3 kernels (gemm3.hip launch_gemm3 encoding) for one problem.
 
@@ -246,29 +281,11 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     im2col_gen = KW * C < 8 and W != KW and KH > 1
     if mode == MODE_WGRAD:
         bmf = 16 if M <= 16 else (32 if M <= 32 else 64)
-        if 64 < M <= 192 and N > 16 and _WGRAD_WIDE == "8":
-            # one f tile per layer up to 192 units (merged Dense): the X panel is read once instead of
-            # once per 64-row f tile and no mostly-empty last f tile is computed; 8 waves per block (2 x 4)
-            # keep the per-thread accumulators and load registers at the 64-row tile's level (+500)
-            bmf = 128 if M <= 128 else (160 if M <= 160 else 192)
-            bnk = 128 if N > 64 and bmf < 192 else 64        # 192 x 128 spills registers
-            return bmf * 1000 + bnk + 500 + (1000000 if im2col_gen else 0)
-        if 64 < M <= 160 and N > 16 and _WGRAD_WIDE == "4":
-            # the same with 4 waves: at one wave per SIMD (241-256 VGPRs) it measured slower than 64-row
-            # tiles on the bench population (1.51 -> 2.22 ms per step, profiles/r2_wide_ab.txt)
-            bmf = 128 if M <= 128 else 160
-            return bmf * 1000 + (128 if N > 64 else 64) + (1000000 if im2col_gen else 0)
+        # (wider f tiles -- 96-row, 128 / 160 / 192-row with 4 or 8 waves -- and 32-row tail tiles were
+        # measured slower on the bench population in round 2 and removed: profiles/r2e/ab_wgrad96.txt,
+        # ab_wgrad_tail32.txt, profiles/r2_wide_ab.txt)
         if N <= 16:                      # narrow reduction width: waves split f, one 16-column tile
             return 64 * 1000 + 16 + (1000000 if im2col_gen else 0)
-        if 64 < M <= 96 and _WGRAD_96:
-            # Dense units just above 64 (the generator's N(64, 8) / N(64, 15) draws): one 96-row f tile
-            # instead of a full 64-row tile plus a mostly empty second one (X read once, 25 % fewer MFMAs)
-            return 96 * 1000 + 64 + (1000000 if im2col_gen else 0)
-
-        if bmf == 64 and _WGRAD_TAIL32 and (64 < M <= 96 or 128 < M <= 160):
-            # a last 64-row f tile that would be mostly empty: 32-row tiles compute 96 / 160 rows
-            # instead of 128 / 192 (at the cost of more re-reads of the X panel)
-            bmf = 32
         if bmf == 16:
             bnk = 256 if N > 128 else (128 if N > 64 else 64)
         else:
@@ -324,23 +341,6 @@ def conv_lds_config(geo: dict, N: int):
             if need <= cap:
                 return rt, tier
     return None
-
-
-def dgrad_as_fwd_conv(r: dict):
-    """DGRAD row of a stride-1 KHxKW > 1 convolution without an activation on its output -> the
-    equivalent FWD-halo row (GF_VPAD): a valid conv of dZ zero-padded by (KH-1, KW-1) with the flipped,
-    transposed weights Wt[C][KH][KW][F] (the row's ``b``).  None when the layer does not qualify.
-    Opt-in (SERANN_DGRAD_HALO=1): measured slower than the register-fragment DGRAD on population B
-    (conv DGRAD 2.66 -> 3.38 ms per step, step 20.07 -> 20.63 ms; profiles/r2e/ab_dgrad_halo.txt) --
-    the halo tiling was tuned for FWD shapes (few input channels, many filters), DGRAD has the reverse."""
-    KH, KW, SH, SW = (int(r.get(k, 1)) for k in ("KH", "KW", "SH", "SW"))
-    if not _DGRAD_HALO or KH * KW <= 1 or SH != 1 or SW != 1 or int(r.get("act", 0)) != 0:
-        return None
-    OH, OW, F, C = int(r["OH"]), int(r["OW"]), int(r["F"]), int(r["C"])
-    t = dict(r)
-    t.update(H=OH + 2 * (KH - 1), W=OW + 2 * (KW - 1), C=F, OH=int(r["H"]), OW=int(r["W"]), F=C, bias=0, act=0,
-             aux=0, flags=(int(r.get("flags", 0)) & GF_ACCUM) | GF_VPAD)
-    return t
 
 
 def conv_wgrad_ipc(geo: dict, tier: int) -> int:
@@ -469,7 +469,10 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 r["b"] = r["_bnat"]
                 r["ldb"] = int(r.get("_bnat_ld", 0))
             if mode == MODE_FWD and splitk:
-                ns = tiled_fwd_splits(M, N, K, v - 7000, int(r.get("flags", 0)))
+                # (split count from the problem's own column tile, not the launch's shared width below:
+                # the split boundaries decide the fp32 partial sums, so they must not depend on the
+                # other problems of the launch)
+                ns = tiled_fwd_splits(M, N, K, tiled_bn(N), int(r.get("flags", 0)))
                 if ns > 1:
                     r["_split"] = ns
         elif mode == MODE_FWD and not (r.get("flags", 0) & GF_ACCUM):
@@ -477,22 +480,12 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             if cfg is not None:
                 nt = 1 if N <= 16 else (2 if N <= 32 else 4)
                 v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
-        if mode == MODE_DGRAD and v is None:
-            vr = dgrad_as_fwd_conv(r)
-            if vr is not None:
-                cfg = conv_lds_config(vr, N)
-                if cfg is not None:
-                    r = vr
-                    nt = 1 if N <= 16 else (2 if N <= 32 else 4)
-                    v = 2000 + nt + 10 * cfg[0] + 100 * cfg[1]
         if mode == MODE_WGRAD and v is None:
             cfg = conv_wgrad_config(r, M)
             if cfg is not None:
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
-        if int(r.get("flags", 0)) & GF_EPI_DACT and not (7000 < v < 9000):
-            raise ValueError("GF_EPI_DACT needs the LDS-tiled DGRAD kernel (K > 32, 1x1)")
         groups.setdefault(v, []).append((r, dm))
     _merge_tiled_widths(groups)
     out = []
@@ -546,14 +539,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             bm, bn = gemm3_block(mode, v)
             dms = [dm for _, dm in items]
             if mode == MODE_WGRAD:
-                tg = [wgrad_target(M, N) for (M, N, K) in dms]
+                tg = [wgrad_target(M, N, K, bm, bn) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
-                # a launch of few blocks leaves most of the 256 CUs idle (measured: 57 blocks for two
-                # [70 x 98] Dense WGRADs over 75000 rows ran at 0.2 TB/s): split the reductions finer
-                # until the launch fills the GPU (the extra fp32 atomics are per-block output tiles)
-                while len(tiles) < WGRAD_MIN_BLOCKS and max(tg) > 16 and "wgrad_minblocks" not in _OFF:
-                    tg = [max(16, t_ // 2) for t_ in tg]
-                    tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
@@ -600,19 +587,13 @@ def tiled_fwd_splits(M: int, N: int, K: int, bn: int, flags: int) -> int:
     rows, N <= 256) and a long reduction (K up to ~20k): unsplit, a handful of blocks each walk hundreds
     of latency-bound k steps.  Split so every block walks about SPLIT_KSTEPS k steps (at most 16
     splits); bf16 problems only (GF_OUT_F32 / GF_ACCUM outputs are never split)."""
-    if SPLIT_KSTEPS <= 0 or flags & (GF_OUT_F32 | GF_ACCUM | GF_SPLITK):
+    if SPLIT_KSTEPS <= 0 or flags & (GF_OUT_F32 | GF_ACCUM):
         return 1
     kt = -(-K // BK)
     tiles = -(-M // 128) * -(-N // bn)
     if tiles >= 256 or kt < 2 * SPLIT_KSTEPS:
         return 1
     return int(min(16, kt // SPLIT_KSTEPS))
-
-
-def gemm2_block(mode: int, variant: int):
-    if mode == MODE_WGRAD:
-        return (variant, 64)
-    return (32, variant % 1000) if variant >= 1000 else (128, variant)
 
 
 def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
@@ -623,22 +604,22 @@ def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
     return max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps), _WGRAD_MAXSPLIT))
 
 
-def wgrad_target(M: int, N: int) -> int:
-    """k-steps (32 rows) per WGRAD block: small weight matrices split the reduction finer (more
-    parallelism, negligible atomic traffic); large ones keep long blocks (fewer fp32 atomics)."""
-    return _WGRAD_TARGET
+def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
+    """k-steps (32 rows) per WGRAD block: SERANN_WGRAD_TARGET (128), halved (down to 16) while the
+    problem alone has fewer than WGRAD_MIN_BLOCKS blocks -- a small weight matrix over many rows
+    (measured: two [70 x 98] Dense WGRADs over 75000 rows in 57 blocks ran at 0.2 TB/s) splits its
+    reduction finer.  A function of the problem alone: the m-split boundaries decide the fp32 partial
+    sums that meet in the fixed-point arena, so they must not depend on the launch (deterministic
+    sharding)."""
+    tg = _WGRAD_TARGET
+    tiles = -(-int(M) // bm) * -(-int(N) // bn)
+    while tg > 16 and K and tiles * wgrad_splits(K, tg, min(32, tg)) < WGRAD_MIN_BLOCKS:
+        tg //= 2
+    return tg
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
-WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "512"))    # per grouped launch
-# 96-row f tile for 64 < F <= 96: opt-in, measured slower (population B step 19.9 -> 29.1 ms: the
-# 96-row blocks drop to 2 waves per SIMD and stage 4 A passes per step; profiles/r2e/ab_wgrad96.txt)
-_DGRAD_HALO = _os.environ.get("SERANN_DGRAD_HALO", "0") == "1"   # DGRAD of stride-1 convs on the halo kernel
-# 32-row f tiles for F in (64, 96] / (128, 160] (fewer computed rows, more X re-reads): opt-in, measured
-# slower (population B step 20.0 -> 20.5 ms, 593 -> 615 launches; profiles/r2e/ab_wgrad_tail32.txt)
-_WGRAD_TAIL32 = _os.environ.get("SERANN_WGRAD_TAIL32", "0") == "1"
-_WGRAD_96 = _os.environ.get("SERANN_WGRAD_96", "0") == "1"
-_WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0")   # "8": 8-wave wide f tiles, "4": 4-wave, "0": off (both measured slower)
+WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 

@@ -2,9 +2,9 @@
 evolutionary_experiment/logic/ribosomal_autoencoder.py:116-124).
 
 * Decode (K33-K35): genotype bits -> token ids.  Eval-mode BatchNormalization layers are folded into
-  the preceding Conv1D / Dense weights, so decode is two grouped MFMA GEMM launches (Conv1D 2->32 k5 as
-  an implicit-GEMM conv; Dense 3072 -> 350*V with fp32 output) and one fused group-argmax launch.
-  log_softmax is monotone, so it is never materialised.
+  the preceding Conv1D / Dense weights, so decode is two gemm3 MFMA launches (Conv1D 2->32 k5 on the
+  LDS-halo implicit-GEMM conv kernel; Dense 3072 -> 350*V on the LDS-tiled kernel with fp32 output) and
+  one fused group-argmax launch.  log_softmax is monotone, so it is never materialised.
 * Training (K37): ``categorical_loglik`` -- log-softmax over the vocabulary, gather at the target
   tokens and the sum over the sequence in one HIP kernel (and its backward), instead of materialising
   the [B][L][V] log-probabilities (model.py:45-46, 54-59).
@@ -12,7 +12,8 @@ evolutionary_experiment/logic/ribosomal_autoencoder.py:116-124).
   embedding is folded into the embedding table, the BatchNormalizations after the three Conv2Ds into
   their weights and biases.  Encode is an embedding-gather launch, three LDS-halo MFMA convolutions
   (350x50x1 -> 346x46x32 -> 344x44x16 -> 342x42x16, NHWC bf16), the split-K LDS-tiled Dense
-  229,824 -> 200 (fp32 atomics, K >> M, N) and a group-argmax over the alphabet.
+  229,824 -> 200 (K >> M, N: per-split fp32 partial slabs + an ordered finalize, no atomics, so encode is
+  deterministic) and a group-argmax over the alphabet.
 """
 from __future__ import annotations
 
@@ -52,41 +53,49 @@ class HipRiboDecoder:
             self.w2 = w2.to(self.device, torch.bfloat16).contiguous()
             self.b2 = b2.to(self.device, torch.float32).contiguous()
         self.C1 = w.shape[0]
+        self._plans = {}
 
     def stale(self, model) -> bool:
         return id(model) != self.model_id or getattr(model, "_param_version", 0) != self.version
 
-    def _desc(self, row):
-        a = np.zeros(1, dtype=H.GEMM_DTYPE)
-        for k, v in row.items():
-            a[0][k] = v
-        return torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=self.device)
+    def _plan(self, B: int):
+        """Buffers and gemm3 launches for a batch of B genotypes (cached per B)."""
+        if B in self._plans:
+            return self._plans[B]
+        G, A, V, L, C1 = self.G, self.A, self.V, self.L, self.C1
+        OL, dev = G - 4, self.device
+        x = torch.zeros(B * G * A + 64, dtype=torch.bfloat16, device=dev)
+        h = torch.zeros(B * OL * C1 + 64, dtype=torch.bfloat16, device=dev)
+        logits = torch.empty(B, L * V, dtype=torch.float32, device=dev)
+        out = torch.empty(B, L, dtype=torch.int32, device=dev)
+        K1, K2 = 5 * A, OL * C1
+        launches = []
+        for row, dims in ((dict(a=x.data_ptr(), b=self.w1.data_ptr(), out=h.data_ptr(), bias=self.b1.data_ptr(),
+                                H=G, W=1, C=A, OH=OL, OW=1, F=C1, KH=5, KW=1, SH=1, SW=1, M=B * OL, N=C1, K=K1,
+                                act=0, flags=(H.GF_VEC_B if K1 % 8 == 0 else 0)), (B * OL, C1, K1)),
+                          (dict(a=h.data_ptr(), b=self.w2.data_ptr(), out=logits.data_ptr(), bias=self.b2.data_ptr(),
+                                H=1, W=1, C=K2, OH=1, OW=1, F=L * V, KH=1, KW=1, SH=1, SW=1, M=B, N=L * V, K=K2,
+                                act=0, flags=H.GF_OUT_F32 | (H.GF_VEC_A | H.GF_VEC_B if K2 % 8 == 0 else 0)),
+                           (B, L * V, K2))):
+            for v, rws, tiles in H.gemm3_plan(H.MODE_FWD, [row], [dims]):
+                d = torch.as_tensor(np.frombuffer(H.gemm_desc_array(rws).tobytes(), dtype=np.uint8).copy(), device=dev)
+                launches.append((v, d, torch.as_tensor(np.ascontiguousarray(tiles), device=dev)))
+        pl = dict(x=x, h=h, logits=logits, out=out, launches=launches)
+        self._plans[B] = pl
+        return pl
 
     @torch.no_grad()
     def __call__(self, bits: torch.Tensor) -> torch.Tensor:
         B = bits.shape[0]
-        G, A, V, L, C1 = self.G, self.A, self.V, self.L, self.C1
-        OL = G - 4
+        pl = self._plan(B)
         lib, s = H.lib(), H.stream_handle()
-        x = torch.nn.functional.one_hot(bits.to(self.device).long(), A).to(torch.bfloat16).contiguous()
-        h = torch.empty(B, OL, C1, dtype=torch.bfloat16, device=self.device)
-        logits = torch.empty(B, L * V, dtype=torch.float32, device=self.device)
-        out = torch.empty(B, L, dtype=torch.int32, device=self.device)
-        K1 = 5 * A
-        d1 = self._desc(dict(a=x.data_ptr(), b=self.w1.data_ptr(), out=h.data_ptr(), bias=self.b1.data_ptr(),
-                             H=G, W=1, C=A, OH=OL, OW=1, F=C1, KH=5, KW=1, SH=1, SW=1, M=B * OL, N=C1, K=K1,
-                             act=0, flags=(H.GF_VEC_B if K1 % 8 == 0 else 0)))
-        t1 = torch.as_tensor(H.gemm_tiles([(B * OL, C1, K1)], H.MODE_FWD), device=self.device)
-        lib.grouped_gemm(H.MODE_FWD, d1.data_ptr(), t1.data_ptr(), len(t1), s)
-        K2 = OL * C1
-        d2 = self._desc(dict(a=h.data_ptr(), b=self.w2.data_ptr(), out=logits.data_ptr(), bias=self.b2.data_ptr(),
-                             H=1, W=1, C=K2, OH=1, OW=1, F=L * V, KH=1, KW=1, SH=1, SW=1, M=B, N=L * V, K=K2,
-                             act=0, flags=H.GF_OUT_F32 | (H.GF_VEC_A if K2 % 8 == 0 else 0) |
-                             (H.GF_VEC_B if K2 % 8 == 0 else 0)))
-        t2 = torch.as_tensor(H.gemm_tiles([(B, L * V, K2)], H.MODE_FWD), device=self.device)
-        lib.grouped_gemm(H.MODE_FWD, d2.data_ptr(), t2.data_ptr(), len(t2), s)
-        lib.group_argmax(logits.data_ptr(), out.data_ptr(), B * L, V, s)
-        return out.long()
+        n = B * self.G * self.A
+        pl["x"][:n].view(B, self.G, self.A).copy_(
+            torch.nn.functional.one_hot(bits.to(self.device).long(), self.A).to(torch.bfloat16))
+        for v, d, t in pl["launches"]:
+            lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
+        lib.group_argmax(pl["logits"].data_ptr(), pl["out"].data_ptr(), B * self.L, self.V, s)
+        return pl["out"].long().clone()
 
 
 def _fold_bn(bn):
@@ -153,12 +162,16 @@ class HipRiboEncoder:
         K = Hh * Ww * C
         N = self.G * self.A
         logits = torch.zeros(B, N, dtype=torch.float32, device=dev)
-        row = dict(a=cur.data_ptr(), b=self.wd.data_ptr(), out=logits.data_ptr(), bias=self.bd.data_ptr(),
-                   H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=B, N=N, K=K, act=0,
-                   flags=H.GF_OUT_F32 | H.GF_SPLITK | (H.GF_VEC_A | H.GF_VEC_B if K % 8 == 0 else 0))
-        d = torch.as_tensor(np.frombuffer(H.gemm_desc_array([row]).tobytes(), dtype=np.uint8).copy(), device=dev)
         kt = -(-K // H.BK)
         per = self.SPLIT_KSTEPS
+        ns = -(-kt // per)
+        # split-K: split s writes its fp32 partial tile to ws[s] (GF_SPLITWS); splitk_finalize sums the
+        # splits in order and adds the bias (deterministic, no atomics)
+        ws = torch.empty(ns * B * N, dtype=torch.float32, device=dev)
+        row = dict(a=cur.data_ptr(), b=self.wd.data_ptr(), out=logits.data_ptr(), bias=0, aux=ws.data_ptr(),
+                   H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=B, N=N, K=K, act=0, kper=per, sbase=0,
+                   flags=H.GF_SPLITWS | (H.GF_VEC_A | H.GF_VEC_B if K % 8 == 0 else 0))
+        d = torch.as_tensor(np.frombuffer(H.gemm_desc_array([row]).tobytes(), dtype=np.uint8).copy(), device=dev)
         tl = []
         for k0 in range(0, kt, per):
             packed = k0 | (min(kt, k0 + per) << 16)
@@ -166,7 +179,12 @@ class HipRiboEncoder:
                 for tn in range(-(-N // 128)):
                     tl.append((0, tm, tn, packed))
         t = torch.as_tensor(np.asarray(tl, dtype=np.int32), device=dev)
-        dense = (7128, d, t)
+        fin = np.zeros(1, dtype=H.SPLITFIN_DTYPE)
+        fin[0] = (ws.data_ptr(), logits.data_ptr(), self.bd.data_ptr(), B, N, ns, 0, 1)
+        fd = torch.as_tensor(np.frombuffer(fin.tobytes(), dtype=np.uint8).copy(), device=dev)
+        ft = torch.as_tensor(H.chunk_tiles([B * N], H.SPLITFIN_ELEMS), device=dev)
+        bufs.append(ws)
+        dense = (7128, d, t, fd, ft)
         bits = torch.empty(B * self.G, dtype=torch.int32, device=dev)
         plan = dict(x=x, bufs=bufs, convs=launches, dense=dense, logits=logits, bits=bits)
         self._plans[B] = plan
@@ -196,9 +214,9 @@ class HipRiboEncoder:
                              self.V, s)
             for v, d, t in pl["convs"]:
                 lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
-            pl["logits"].zero_()
-            v, d, t = pl["dense"]
+            v, d, t, fd, ft = pl["dense"]
             lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
+            lib.splitk_finalize(fd.data_ptr(), ft.data_ptr(), len(ft), s)
             if want_logits:
                 outs.append(pl["logits"].view(B, self.G, self.A).clone())
             else:

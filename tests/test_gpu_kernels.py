@@ -1,7 +1,9 @@
 """Per-kernel numerics on bf16-exact operands vs. plain PyTorch fp32 references of the same op.
 
 Operands are drawn as bf16 values, so the only differences are fp32 accumulation order and the
-final bf16 rounding of the output (<~0.4% relative)."""
+final bf16 rounding of the output (<~0.4% relative).  Gradients land in the deterministic Q32
+fixed-point arena (csrc/hip/common.h fx_*), BatchNorm statistics in the wide fixed-point workspace;
+the determinism tests re-run a kernel and require bitwise-identical results."""
 import math
 
 import numpy as np
@@ -48,29 +50,20 @@ def _desc(rows, dtype):
     return torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=DEV)
 
 
-def _run_gemm(mode, rows, dims, impl="v1"):
+def _run_gemm(mode, rows, dims):
     # reference ops (MIOpen / hipBLASLt) may still be in flight, and the descriptor tables below are
     # uploaded from pageable memory: start every launch from an idle device
     torch.cuda.synchronize()
-    if impl == "v1":
-        d = _desc(rows, H.GEMM_DTYPE)
-        t = torch.as_tensor(H.gemm_tiles(dims, mode), device=DEV)
-        H.lib().grouped_gemm(mode, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
-    elif impl == "v3":
-        for v, rws, tiles in H.gemm3_plan(mode, rows, dims):
-            d = _desc(rws, H.GEMM_DTYPE)
-            t = torch.as_tensor(tiles, device=DEV)
-            H.lib().gemm3(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
-    else:
-        groups = {}
-        for r, dm in zip(rows, dims):
-            groups.setdefault(H.gemm2_variant(mode, dm[0], dm[1], dm[2]), []).append((r, dm))
-        for v, items in groups.items():
-            d = _desc([r for r, _ in items], H.GEMM_DTYPE)
-            bm, bn = H.gemm2_block(mode, v)
-            t = torch.as_tensor(H.gemm_tiles([dm for _, dm in items], mode, bm=bm, bn=bn), device=DEV)
-            H.lib().gemm2(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    for v, rws, tiles in H.gemm3_plan(mode, [dict(r) for r in rows], dims):
+        d = _desc([{k: val for k, val in r.items() if not k.startswith("_")} for r in rws], H.GEMM_DTYPE)
+        t = torch.as_tensor(tiles, device=DEV)
+        H.lib().gemm3(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
     torch.cuda.synchronize()
+
+
+def _q(t):
+    """Q32 fixed-point int64 (gradient arena) -> fp32."""
+    return (t.double() / 2.0 ** 32).float()
 
 
 SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
@@ -109,9 +102,8 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
 ]
 
 
-@pytest.mark.parametrize("impl", ["v1", "v2", "v3"])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
+def test_grouped_conv_fwd_dgrad_wgrad(shape):
     B, Hh, Ww, C, Fo, KH, KW, SH, SW, act = shape
     OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
     g = torch.Generator(device=DEV).manual_seed(0)
@@ -130,50 +122,27 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape, impl):
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=bias.data_ptr(),
                                 M=B * OH * OW, N=Fo, K=K, act=H.ACT_CODES[act], flags=flags, **geo)],
-              [(B * OH * OW, Fo, K)], impl)
+              [(B * OH * OW, Fo, K)])
     assert _rel(y.float(), ref) < 6e-3
     # DGRAD
     dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
     ref_dx = ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     flags = (H.GF_VEC_A if Fo % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-    wt = w.permute(3, 1, 2, 0).contiguous()       # Wt[C][KH][KW][F] for the v2 DGRAD kernel
-    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=(w if impl == "v1" else wt).data_ptr(), out=dx.data_ptr(),
+    wt = w.permute(3, 1, 2, 0).contiguous()       # Wt[C][KH][KW][F] for the register-fragment DGRAD kernel
+    _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), _bnat=w.data_ptr(), out=dx.data_ptr(),
                                   M=B * Hh * Ww, N=C, K=KH * KW * Fo, flags=flags, **geo)],
-              [(B * Hh * Ww, C, KH * KW * Fo)], impl)
+              [(B * Hh * Ww, C, KH * KW * Fo)])
     assert _rel(dx.float(), ref_dx) < 6e-3
-    # WGRAD (accumulates into a zeroed fp32 buffer, split-K)
-    dw = torch.zeros(Fo, KH, KW, C, device=DEV)
+    # WGRAD (accumulates into a zeroed Q32 fixed-point buffer, split over m); run twice: bitwise equal
     ref_dw = ref_conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
-    _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
-                                  flags=flags, **geo)], [(Fo, K, B * OH * OW)], impl)
-    assert _rel(dw, ref_dw) < 2e-5
-
-
-@pytest.mark.parametrize("shape", [s for s in SHAPES if s[5] * s[6] > 1 and s[7] == 1 and s[8] == 1])
-@pytest.mark.parametrize("accum", [False, True])
-def test_dgrad_as_padded_fwd_conv(shape, accum, monkeypatch):
-    """Opt-in DGRAD path (SERANN_DGRAD_HALO=1): a stride-1 conv's DGRAD as a FWD-halo conv of the
-    virtually zero-padded dZ with flipped, transposed weights (GF_VPAD), with and without GF_ACCUM."""
-    monkeypatch.setattr(H, "_DGRAD_HALO", True)
-    B, Hh, Ww, C, Fo, KH, KW, SH, SW, _ = shape
-    OH, OW = Hh - KH + 1, Ww - KW + 1
-    g = torch.Generator(device=DEV).manual_seed(1)
-    w = (torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16()
-    dz = torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16()
-    wr = w.float().permute(0, 3, 1, 2)
-    ref = ref_conv2d_input((B, C, Hh, Ww), wr, dz.float().permute(0, 3, 1, 2), (1, 1)).permute(0, 2, 3, 1)
-    dx = torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16() if accum else \
-        torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
-    if accum:
-        ref = ref + dx.float()
-    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=1, SW=1)
-    wt = w.permute(3, 1, 2, 0).contiguous()
-    rows = [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C, K=KH * KW * Fo,
-                 flags=H.GF_ACCUM if accum else 0, **geo)]
-    plans = H.gemm3_plan(H.MODE_DGRAD, [dict(r) for r in rows], [(B * Hh * Ww, C, KH * KW * Fo)])
-    assert all(2000 <= v < 3000 for v, _, _ in plans)          # took the halo kernel
-    _run_gemm(H.MODE_DGRAD, rows, [(B * Hh * Ww, C, KH * KW * Fo)], "v3")
-    assert _rel(dx.float(), ref) < 6e-3
+    res = []
+    for _ in range(2):
+        dw = torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV)
+        _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
+                                      flags=flags, **geo)], [(Fo, K, B * OH * OW)])
+        res.append(dw)
+    assert torch.equal(res[0], res[1])
+    assert _rel(_q(res[0]), ref_dw) < 2e-5
 
 
 def test_tiled_fwd_split_k_with_finalize():
@@ -264,8 +233,7 @@ def test_transpose_weights_kernel():
     assert torch.equal(out, w.permute(3, 1, 2, 0).contiguous())
 
 
-@pytest.mark.parametrize("impl", ["v1", "v2", "v3"])
-def test_grouped_gemm_many_problems_one_launch(impl):
+def test_grouped_gemm_many_problems_one_launch():
     rows, dims, refs, outs = [], [], [], []
     keep = []
     for i, (B, Hh, Ww, C, Fo, KH, KW, SH, SW, act) in enumerate(SHAPES):
@@ -281,7 +249,7 @@ def test_grouped_gemm_many_problems_one_launch(impl):
         dims.append((B * OH * OW, Fo, K))
         refs.append(ref_conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, (SH, SW)).permute(0, 2, 3, 1))
         outs.append(y)
-    _run_gemm(H.MODE_FWD, rows, dims, impl)
+    _run_gemm(H.MODE_FWD, rows, dims)
     for y, r in zip(outs, refs):
         assert _rel(y.float(), r) < 6e-3
 
@@ -294,11 +262,11 @@ def test_bn_train_infer_backward(RC):
     beta = torch.randn(C, device=DEV)
     mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, invstd = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-    ws = torch.zeros(2 * H.BN_WS_STRIPES * C, device=DEV)
+    ws = torch.zeros(H.bn_ws_words(C), dtype=torch.int64, device=DEV)
     y = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
     dy = torch.randn(R, C, device=DEV).bfloat16()
     dx = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
-    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dg, db = (torch.zeros(C, dtype=torch.int64, device=DEV) for _ in range(2))     # Q32 gradient arena
     row = dict(x=x.data_ptr(), y=y.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), gamma=gamma.data_ptr(),
                beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(), invstd=invstd.data_ptr(),
                ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
@@ -306,9 +274,14 @@ def test_bn_train_infer_backward(RC):
     t = torch.as_tensor(H.chunk_tiles([H.bn_chunks(R, C)], 1), device=DEV)
     ts = torch.as_tensor(H.chunk_tiles([H.bn_chunks(R, C, stats=True)], 1), device=DEV)   # phases 0 / 4
     L, s = H.lib(), H.stream_handle()
-    for ph in (0, 2):
-        tt = ts if ph == 0 else t
-        L.bn(ph, d.data_ptr(), tt.data_ptr(), len(tt), s)
+    L.bn(0, d.data_ptr(), ts.data_ptr(), len(ts), s)
+    torch.cuda.synchronize()
+    ws0 = ws.clone()
+    ws.zero_()
+    L.bn(0, d.data_ptr(), ts.data_ptr(), len(ts), s)        # statistics again: bitwise identical
+    torch.cuda.synchronize()
+    assert torch.equal(ws, ws0)
+    L.bn(2, d.data_ptr(), t.data_ptr(), len(t), s)
     torch.cuda.synchronize()
     xf = x.float().requires_grad_(True)
     g_ = gamma.clone().requires_grad_(True)
@@ -326,7 +299,7 @@ def test_bn_train_infer_backward(RC):
     torch.cuda.synchronize()
     ref.backward(dy.float())
     assert _rel(dx.float(), xf.grad) < 1e-2
-    assert _rel(dg, g_.grad) < 1e-3 and _rel(db, b_.grad) < 1e-3
+    assert _rel(_q(dg), g_.grad) < 1e-3 and _rel(_q(db), b_.grad) < 1e-3
     # inference
     L.bn(3, d.data_ptr(), t.data_ptr(), len(t), s)
     torch.cuda.synchronize()
@@ -368,7 +341,7 @@ def test_loss_kernel_matches_keras_losses():
     labels = torch.randint(0, NC, (B,), device=DEV, dtype=torch.int32)
     tgt = torch.randint(0, 2, (B, L_), device=DEV).bfloat16()
     dz = torch.zeros(B, NC + L_, dtype=torch.bfloat16, device=DEV)
-    metrics = torch.zeros(4, device=DEV)
+    metrics = torch.zeros(4, dtype=torch.int64, device=DEV)          # Q32 fixed point
     lb = 0.3
     row = dict(logits=z.data_ptr(), dlogits=dz.data_ptr(), labels=labels.data_ptr(), target=tgt.data_ptr(),
                metrics=metrics.data_ptr(), NC=NC, L=L_, B=B, lb=lb)
@@ -381,17 +354,17 @@ def test_loss_kernel_matches_keras_losses():
     loss = lb * ce + (1 - lb) * mse
     loss.backward()
     assert _rel(dz.float(), zz.grad) < 6e-3
-    assert abs(metrics[0].item() / B - loss.item()) < 1e-4
-    assert metrics[1].item() == (zz[:, :NC].argmax(1) == labels.long()).sum().item()
-    assert abs(metrics[2].item() / B - mse.item()) < 1e-5
+    m = _q(metrics)
+    assert abs(m[0].item() / B - loss.item()) < 1e-4
+    assert m[1].item() == (zz[:, :NC].argmax(1) == labels.long()).sum().item()
+    assert abs(m[2].item() / B - mse.item()) < 1e-5
 
 
 @pytest.mark.parametrize("shape", [(3, 9, 9, 8, 13, 3, 3), (3, 9, 9, 2, 13, 1, 1), (50, 12, 12, 1, 70, 1, 1)])
-@pytest.mark.parametrize("impl", ["v2", "v3"])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
-def test_fused_act_grad_and_bias_grad(act, impl, shape):
-    """v2/v3 WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient
-    (1x1 shapes with C <= 4 take the v3 narrow VALU kernels)."""
+def test_fused_act_grad_and_bias_grad(act, shape):
+    """WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient
+    (1x1 shapes with C <= 4 take the narrow VALU kernels)."""
     B, Hh, Ww, C, Fo, KH, KW = shape
     SH = SW = 1
     OH, OW = Hh - KH + 1, Ww - KW + 1
@@ -405,11 +378,12 @@ def test_fused_act_grad_and_bias_grad(act, impl, shape):
     dz = dz.bfloat16().float()
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
     K = KH * KW * C
-    dw = torch.zeros(Fo, KH, KW, C, device=DEV)
-    db = torch.zeros(Fo, device=DEV)
+    dw = torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV)
+    db = torch.zeros(Fo, dtype=torch.int64, device=DEV)
     _run_gemm(H.MODE_WGRAD, [dict(a=dy.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), bias=db.data_ptr(),
                                   aux=y.data_ptr(), act=H.ACT_CODES[act], M=Fo, N=K, K=B * OH * OW, **geo)],
-              [(Fo, K, B * OH * OW)], impl)
+              [(Fo, K, B * OH * OW)])
+    dw, db = _q(dw), _q(db)
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)
     ref_dw = ref_conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
@@ -417,15 +391,14 @@ def test_fused_act_grad_and_bias_grad(act, impl, shape):
     assert _rel(db, dz.sum((0, 1, 2))) < 1e-3
     dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
     wt = w.permute(3, 1, 2, 0).contiguous()
-    _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), aux=y.data_ptr(),
-                                  act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
-              [(B * Hh * Ww, C, KH * KW * Fo)], impl)
+    _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), _bnat=w.data_ptr(), out=dx.data_ptr(),
+                                  aux=y.data_ptr(), act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
+              [(B * Hh * Ww, C, KH * KW * Fo)])
     ref_dx = ref_conv2d_input(xr.shape, wr, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref_dx) < 6e-3
 
 
-@pytest.mark.parametrize("impl", ["v2", "v3"])
-def test_wave_split_k_dense(impl):
+def test_wave_split_k_dense():
     """Few rows, long K (the Dense-on-merge shape): the wave-split-K form must match."""
     M, K, N = 750, 5003, 110
     x = torch.randn(M, K, device=DEV).bfloat16()
@@ -433,13 +406,10 @@ def test_wave_split_k_dense(impl):
     b = torch.randn(N, device=DEV)
     y = torch.zeros(M, N, device=DEV)
     geo = dict(H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1)
-    if impl == "v2":
-        assert H.gemm2_variant(H.MODE_FWD, M, N, K) >= 1000
-    else:
-        assert 100 <= H.gemm3_variant(H.MODE_FWD, M, N, K, geo) % 1000
+    assert 100 <= H.gemm3_variant(H.MODE_FWD, M, N, K, geo) % 1000
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), M=M, N=N, K=K,
                                 flags=H.GF_OUT_F32, **geo)],
-              [(M, N, K)], impl)
+              [(M, N, K)])
     assert _rel(y, x.float() @ w.float().t() + b) < 1e-4
 
 
@@ -459,12 +429,12 @@ def test_v3_accumulating_outputs(shape):
     dx = prev.clone()
     wt = w.permute(3, 1, 2, 0).contiguous()
     _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
-                                  K=KH * KW * Fo, flags=H.GF_ACCUM, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)], "v3")
+                                  K=KH * KW * Fo, flags=H.GF_ACCUM, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)])
     ref = prev.float() + ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref) < 6e-3
     prev_y = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
     y = prev_y.clone()
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), M=B * OH * OW, N=Fo,
-                                K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)], "v3")
+                                K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)])
     ref_y = prev_y.float() + ref_conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(y.float(), ref_y) < 6e-3

@@ -37,17 +37,65 @@ def test_tiled_widths_are_shared_per_launch_group():
 
 def test_wgrad_variants_default_to_64_row_tiles():
     assert H.gemm3_variant(H.MODE_WGRAD, 135, 4896, 750, {}) == 64128
-    assert H.gemm3_block(H.MODE_WGRAD, 160628) == (160, 128)
-
-
-def test_wgrad_96_row_tile_is_opt_in(monkeypatch):
-    # F in (64, 96]: 64-row tiles by default; the 96-row tile (measured slower) only behind the switch
+    # F in (64, 96]: 64-row tiles (the 96-row / wide / tail-32 tiles measured slower and were removed)
     assert H.gemm3_variant(H.MODE_WGRAD, 73, 64, 432000, {}) == 64064
-    monkeypatch.setattr(H, "_WGRAD_96", True)
-    assert H.gemm3_variant(H.MODE_WGRAD, 73, 64, 432000, {}) == 96064
-    assert H.gemm3_block(H.MODE_WGRAD, 96064) == (96, 64)
-    assert H.gemm3_variant(H.MODE_WGRAD, 64, 64, 432000, {}) == 64064
     assert H.gemm3_variant(H.MODE_WGRAD, 97, 64, 432000, {}) == 64064
+
+
+def _split_signature(mode, rows, dims):
+    """Per problem: the k ranges / row blocks its blocks cover (what decides its fp32 partial sums)."""
+    out = {}
+    for v, rws, tiles in H.gemm3_plan(mode, [dict(r) for r in rows], dims, splitk=True):
+        for p, r in enumerate(rws):
+            t = tiles[tiles[:, 0] == p]
+            key = r["out"]
+            out[key] = (sorted(set(int(x) for x in t[:, 3])), int(r.get("_split", 1)), int(r.get("flags", 0)) & H.GF_WSTORE)
+    return out
+
+
+def test_decomposition_is_per_problem():
+    """Deterministic sharding: a problem's reduction splits (WGRAD m-splits, FWD k-splits, fused-chain row
+    blocks, conv+pool images per block) are the same alone as inside any grouped launch, so an organism
+    trains bit-identically whatever shard / stream group it lands in."""
+    geo = dict(H=1, W=1, OH=1, OW=1, KH=1, KW=1, SH=1, SW=1)
+    wg = [dict(a=0, b=0, out=1000 + i, C=K, F=F, M=F, N=K, K=R, flags=0, **geo)
+          for i, (F, K, R) in enumerate([(70, 98, 75000), (128, 300, 750), (16, 40, 588000), (64, 3000, 96000)])]
+    wdims = [(r["M"], r["N"], r["K"]) for r in wg]
+    full = _split_signature(H.MODE_WGRAD, wg, wdims)
+    for r, d in zip(wg, wdims):
+        assert _split_signature(H.MODE_WGRAD, [r], [d])[r["out"]] == full[r["out"]]
+    fw = [dict(a=0, b=0, out=2000 + i, C=K, F=N, M=750, N=N, K=K, act=0, flags=H.GF_VEC_A | H.GF_VEC_B, **geo)
+          for i, (N, K) in enumerate([(135, 12000), (200, 6000), (40, 9000), (190, 2100)])]
+    fdims = [(750, r["N"], r["K"]) for r in fw]
+    full = _split_signature(H.MODE_FWD, fw, fdims)
+    for r, d in zip(fw, fdims):
+        assert _split_signature(H.MODE_FWD, [r], [d])[r["out"]] == full[r["out"]]
+    # fused chain and conv+pool: functions of the problem alone
+    assert H.gchain_rpb(72000, H.GC_BFULL, 96, 100) == H.gchain_rpb(72000, H.GC_BFULL, 96, 100)
+    assert H.convpool_wgrad_imgs(750, 32) == 32 and H.convpool_wgrad_imgs(80, 16) == 8
+
+
+def test_gchain_large_genotype_is_not_fused():
+    """A fused chain stages the genotype rows of a block in LDS (GCHAIN_GMAX elements); chains whose
+    smallest block (64 rows) cannot fit stay on the unfused kernels (advisor finding, round 2)."""
+    assert H.gchain_fits(96, 100)
+    assert not H.gchain_fits(1, 8192)            # 65 batch rows x 8192 genotype elements
+    with pytest.raises(ValueError):
+        H.gchain_rpb(64 * 1000, H.GC_FSTAT, 1, 8192)
+    src = ("g_layer=Conv1D(filters=8,kernel_size=3,strides=2)(g_layer)\n"
+           "g_layer=Dense(units=16,activation='relu')(g_layer)\n"
+           "con=concatenate([Reshape((1,-1))(X_layer),Reshape((1,-1))(g_layer)])\n"
+           "loss_balance=0.5")
+    from serann.engine.hip_engine import gchain_triples
+    assert gchain_triples(interpret(src, genotype_size=100))
+    assert not gchain_triples(interpret(src, genotype_size=16000))
+
+
+def test_convpool_pool_window_limit():
+    """The fused conv+pool kernel packs the pool-window offset into 8 bits: at most 256 windows."""
+    assert H.convpool_ok(28, 28, 5, 5, 2, 2)
+    assert H.convpool_ok(28, 28, 3, 3, 16, 16)
+    assert not H.convpool_ok(28, 28, 3, 3, 17, 16)
 
 
 @pytest.mark.parametrize("name,fused", [("convpool_bench_a", True), ("convpool_k9_f80", True),
@@ -102,8 +150,8 @@ def test_gchain_variant_and_block_sizing():
     assert H.gchain_variant(16, 129, 3) is None          # F2 > 128
     assert H.gchain_variant(16, 64, 17) is None          # > 16 taps
     for mode in range(4):
-        for rows, l1, nprob in ((72000, 96, 112), (750, 1, 3), (8000, 100, 1), (363000, 484, 2)):
-            rpb = H.gchain_rpb(rows, nprob, mode, l1, 100)
+        for rows, l1 in ((72000, 96), (750, 1), (8000, 100), (363000, 484)):
+            rpb = H.gchain_rpb(rows, mode, l1, 100)
             assert rpb % 64 == 0 and rpb >= 64
             # the block's genotype rows fit the kernel's LDS staging buffer
             assert (-(-rpb // l1) + 1) * 100 <= H.GCHAIN_GMAX
