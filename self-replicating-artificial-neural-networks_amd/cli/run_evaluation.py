@@ -60,7 +60,9 @@ def update_workers_with_cached_evaluations(evaluations_path, df, worker):
 def main(argv=None, script=None):
     args = get_args(argv)
     from .launch import maybe_relaunch
-    maybe_relaunch(args, script or __file__)
+    from pathlib import Path
+    maybe_relaunch(args, script or str(Path(__file__).resolve().parents[2] / "serann_evaluation" / "run_evaluation.py"),
+                   argv, resume=False)
 
     from ..analysis.results import load_experiment_results
     from ..config import experiment_config as config

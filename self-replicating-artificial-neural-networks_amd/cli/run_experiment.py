@@ -36,8 +36,9 @@ def get_args(argv=None):
 
 def main(argv=None, script=None):
     args = get_args(argv)
-    from .launch import maybe_relaunch
-    maybe_relaunch(args, script or __file__)
+    from .launch import maybe_relaunch, record_run_id
+    maybe_relaunch(args, script or str(Path(__file__).resolve().parents[2] / "evolutionary_experiment" /
+                                       "run_experiment.py"), argv)
 
     from ..config import experiment_config as config
     from ..experiment.experiment import Experiment
@@ -97,6 +98,7 @@ def main(argv=None, script=None):
     parameters["ribosomal_autoencoder"] = s.codec.get_model_name()
     parameters["random_seed"] = seed
     if comm.is_root:
+        record_run_id(experiment_id)
         print(f"Experiment id: {experiment_id} | ranks: {comm.world_size} | engine: {s.engine} | "
               f"codec: {s.codec.get_model_name()} | data: {'synthetic' if s.data.synthetic else 'MNIST'}", flush=True)
     exp = Experiment(experiment_id, s.encodings, s.worker, db, parameters, s.codec, comm=comm,

@@ -6,9 +6,12 @@ Three tiers are kept: (1) python dicts with the same keys as the reference,
 overridden with ``SERANN_ROOT`` (project root) or per-key environment variables
 ``SERANN_<KEY_UPPER>``.
 
-``max_serann_per_gpu`` is no longer a hard V100-era constant: it is derived from
-HBM capacity by :func:`max_serann_per_gpu` (288 GB per MI355X), but the key is
-kept for compatibility.
+``max_serann_per_gpu`` (112, a V100-era job size) is kept as a key for compatibility
+but not applied: a rank trains its whole shard at once when it fits in HBM and in
+waves sized from each organism's estimated device bytes otherwise
+(:mod:`serann.experiment.capacity`).  ``worker_pool_job_timeout`` is the
+per-generation watchdog timeout (:class:`serann.utils.faults.GenerationWatchdog`)
+and sets the collective timeout.
 """
 from __future__ import annotations
 
@@ -86,18 +89,3 @@ def load_parameters(path) -> dict:
 
 def default_parameters(name: str = "example") -> dict:
     return load_parameters(PARAMETERS_DIR / "experiment" / f"{name}.json")
-
-
-HBM_BYTES_PER_GPU = 288e9
-
-
-def max_serann_per_gpu(train_batch: int = 750, hbm_bytes: float = HBM_BYTES_PER_GPU,
-                       bytes_per_organism: float | None = None) -> int:
-    """HBM-derived organism capacity of one MI355X.
-
-    The p99 organism keeps < 300 MB of bf16 activations + fp32 weights/Adam state
-    at batch 750 (derived from the generator distribution); we budget 60 % of HBM.
-    """
-    if bytes_per_organism is None:
-        bytes_per_organism = 300e6 * (train_batch / 750.0)
-    return max(1, int(0.6 * hbm_bytes / bytes_per_organism))

@@ -34,7 +34,7 @@ import pandas as pd
 from ..genome.interpreter import layer_counts
 from ..parallel.comm import Comm, LocalComm, pack_results, unpack_results
 from ..parallel.partition import lpt_partition
-from ..utils.faults import maybe_inject
+from ..utils.faults import GenerationWatchdog, maybe_inject
 from ..utils.levenshtein import levenshtein_batch
 from ..utils.stats import fertility, genotype_stats, source_code_stats
 from ..utils.trace import PhaseTimer, phase
@@ -54,7 +54,7 @@ class Experiment:
     def __init__(self, experiment_id: str, serann_dataset: np.ndarray, worker: ShardWorker, experiment_db,
                  parameters: dict, codec, comm: Optional[Comm] = None, start_generation: int = 0,
                  random_seed: int = 0, strict_reference: bool = False, verbose: bool = True,
-                 perf_log: Optional[str] = None):
+                 perf_log: Optional[str] = None, job_timeout: Optional[float] = None):
         self._id = experiment_id
         self._serann_dataset = serann_dataset
         self._worker = worker
@@ -72,6 +72,11 @@ class Experiment:
                                      int(parameters["genotype_size"]),
                                      int(parameters["num_classification_classes"]))
         self.history: List[dict] = []
+        if job_timeout is None:
+            from ..config import experiment_config
+            job_timeout = float(experiment_config["worker_pool_job_timeout"])
+        # per-generation job timeout (the reference pool's worker_pool_job_timeout, config.py:7)
+        self._watchdog = GenerationWatchdog(job_timeout, self._comm.rank)
         if self._comm.is_root and self._db is not None:
             self._db.save_execution_info(datetime.now(), self._parameters)
 
@@ -100,16 +105,20 @@ class Experiment:
             generation_start_time = datetime.now()
             t0 = time.perf_counter()
             self.log(f"### Generation {generation_number} execution has started ###")
-            maybe_inject(generation_number, self._comm.rank)          # SERANN_FAULT_INJECT (recovery tests)
             timer = PhaseTimer()
             current["experiment_id"] = self._id
             current["generation"] = generation_number
             current["num_offspring"] = 0
 
             self.log("Starting training and replication")
-            with phase("learn_and_replicate", timer):
-                models_info, offspring_by_id, times = self._learn_and_replicate(current, offspring_pool_size,
-                                                                               generation_number)
+            self._watchdog.arm(f"generation {generation_number}")
+            try:
+                maybe_inject(generation_number, self._comm.rank)      # SERANN_FAULT_INJECT (recovery tests)
+                with phase("learn_and_replicate", timer):
+                    models_info, offspring_by_id, times = self._learn_and_replicate(current, offspring_pool_size,
+                                                                                   generation_number)
+            finally:
+                self._watchdog.disarm()
             current = current.join(models_info)
 
             self.log("Calculating fecundity scores")

@@ -77,6 +77,8 @@ def setup(parameters: dict, engine: str = "auto", codec: str = "auto", comm: Opt
           train_cfg: Optional[TrainConfig] = None, table_size: int = 4096) -> Setup:
     comm = comm or make_comm()
     device = device or default_device(comm)
+    from .capacity import admit
+    admit(device)                       # GPU-memory admission (reference run_experiment.py:103)
     if engine == "auto":
         engine = default_engine(device)
     encodings = load_encodings(genotype_size=int(parameters["genotype_size"]))

@@ -4,19 +4,23 @@ Reference: ``EvolutionaryExperimentWorker.run`` (evolutionary_experiment/logic/e
 45-167).  For its shard of *trainable* organisms a rank builds one population engine, trains it
 jointly (``fit``), evaluates on the test set and replicates each organism on its own rows.
 Interpretation (validity / parameter count / overweight) is done by the replicated control plane
-(:mod:`serann.experiment.population`), so the worker only sees trainable organisms.
+(:mod:`serann.experiment.population`), so the worker only sees trainable organisms.  Shards larger
+than the device budget train in waves with an out-of-memory fallback (:mod:`serann.experiment.capacity`,
+replacing the reference's 112-organism jobs and half-batch retry, experiment_worker.py:121-126).
 """
 from __future__ import annotations
 
+import dataclasses
 import hashlib
 import time
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
 from ..engine.base import TrainConfig, replication_image_rows
 from ..genome.ir import OrganismIR
+from . import capacity
 
 
 def replication_bits(outputs: np.ndarray) -> np.ndarray:
@@ -57,20 +61,27 @@ class ShardResult:
 
 class ShardWorker:
     def __init__(self, parameters: dict, data, engine: str = "torch", device="cpu",
-                 train_cfg: Optional[TrainConfig] = None):
+                 train_cfg: Optional[TrainConfig] = None, max_per_wave: Optional[int] = None,
+                 log: Optional[Callable[[str], None]] = None):
         self.params = parameters
         self.data = data
         self.engine_name = engine
         self.device = device
         self.cfg = train_cfg or TrainConfig(epochs=int(parameters["training_epochs"]),
                                             batch_size=int(parameters["training_batch_size"]))
+        self.max_per_wave = max_per_wave
+        self.log = log or (lambda m: print(m, flush=True))
+        self.last_waves: List[List[int]] = []        # (introspection: tests, perf log)
 
     def run(self, indices: Sequence[int], ids: Sequence[str], genotypes: np.ndarray, irs: List[OrganismIR],
             num_replications: int, generation: int, random_seed: int,
             positions: Optional[Sequence[int]] = None, n_trainable: Optional[int] = None) -> ShardResult:
         """``positions``/``n_trainable``: the organisms' positions among *all* trainable organisms of
         the generation, which fixes their replication images independently of the partition (the
-        reference's single-job layout, experiment_worker.py:140-160)."""
+        reference's single-job layout, experiment_worker.py:140-160).
+
+        The shard is trained in one engine when it fits the rank's device budget, else in waves
+        (:mod:`serann.experiment.capacity`); an out-of-memory error splits a wave and retries."""
         n = len(indices)
         L = int(self.params["genotype_size"])
         if n == 0:
@@ -79,26 +90,55 @@ class ShardWorker:
         cfg = self.cfg
         cfg.seed = int(hashlib.blake2b(f"{random_seed}:{generation}:perm".encode(), digest_size=4).hexdigest(), 16)
         seeds = [organism_seed(random_seed, generation, i) for i in ids]
-        engine = make_engine(self.engine_name, irs, seeds, self.device, cfg)
-        try:
-            fit = engine.fit(self.data, cfg)
-            d = self.data
-            test_acc = engine.evaluate(d.test_x, d.test_labels, d.test_g, cfg)
-            learning_time = fit.learning_time
+        d = self.data
+        pos = list(range(n)) if positions is None else list(positions)
+        total = (n if n_trainable is None else n_trainable) * num_replications
+        genotypes = np.asarray(genotypes, np.float32)
 
-            offspring = np.zeros((n, num_replications, L), np.uint8)
-            replication_time = 0.0
-            if num_replications > 0:
-                t0 = time.perf_counter()
-                pos = list(range(n)) if positions is None else list(positions)
-                total = (n if n_trainable is None else n_trainable) * num_replications
-                images = [d.test_x[replication_image_rows(q, num_replications, total, len(d.test_x))]
-                          for q in pos]
-                outs = engine.replicate(np.asarray(genotypes, np.float32), images, cfg)
-                for p, o in enumerate(outs):
-                    offspring[p] = replication_bits(o)
-                replication_time = time.perf_counter() - t0
-        finally:
-            engine.close()
-        metrics = np.stack([fit.val_acc, fit.train_acc, test_acc, fit.val_mse], axis=1).astype(np.float64)
-        return ShardResult(np.asarray(indices, np.int32), metrics, offspring, learning_time, replication_time)
+        budget = capacity.device_budget(self.device)
+        sizes = [capacity.organism_device_bytes(ir, cfg.batch_size, min(num_replications, cfg.batch_size))
+                 for ir in irs]
+        waves = capacity.plan_waves(sizes, budget, self.max_per_wave)
+        self.last_waves = []
+        if len(waves) > 1:
+            self.log(f"shard of {n} organisms (~{sum(sizes) / 1e9:.1f} GB) trained in {len(waves)} waves "
+                     f"(budget {budget / 1e9:.1f} GB)" if budget else f"shard of {n} organisms in {len(waves)} waves")
+
+        metrics = np.full((n, 4), np.nan)
+        offspring = np.zeros((n, num_replications, L), np.uint8)
+        times = [0.0, 0.0]
+
+        def run_wave(members: List[int], batch: Optional[int]):
+            wcfg = cfg if batch is None else dataclasses.replace(cfg, batch_size=int(batch))
+            engine = make_engine(self.engine_name, [irs[i] for i in members], [seeds[i] for i in members],
+                                 self.device, wcfg)
+            try:
+                fit = engine.fit(d, wcfg)
+                test_acc = engine.evaluate(d.test_x, d.test_labels, d.test_g, wcfg)
+                outs, rt = None, 0.0
+                if num_replications > 0:
+                    t0 = time.perf_counter()
+                    images = [d.test_x[replication_image_rows(pos[i], num_replications, total, len(d.test_x))]
+                              for i in members]
+                    outs = engine.replicate(genotypes[members], images, wcfg)
+                    rt = time.perf_counter() - t0
+            finally:
+                engine.close()
+            return members, fit, test_acc, outs, fit.learning_time, rt
+
+        def on_fail(members: List[int]):
+            return members, None, None, None, 0.0, 0.0
+
+        for w in waves:
+            for members, fit, test_acc, outs, lt, rt in capacity.run_with_fallback(
+                    w, run_wave, cfg.batch_size, self.device, self.log, on_fail):
+                self.last_waves.append(list(members))
+                times[0] += lt
+                times[1] += rt
+                if fit is None:
+                    continue                               # did not fit even at half batch: NaN metrics
+                metrics[members] = np.stack([fit.val_acc, fit.train_acc, test_acc, fit.val_mse], axis=1)
+                if outs is not None:
+                    for k, o in zip(members, outs):
+                        offspring[k] = replication_bits(o)
+        return ShardResult(np.asarray(indices, np.int32), metrics.astype(np.float64), offspring, times[0], times[1])

@@ -59,11 +59,13 @@ class TorchDistComm(Comm):
     """torch.distributed communicator.  Uses byte tensors so that one all-gather moves all
     of a rank's results; on RCCL the tensors are device tensors (no host staging in RCCL)."""
 
-    def __init__(self, backend: Optional[str] = None, device=None, timeout_s: int = 1800):
+    def __init__(self, backend: Optional[str] = None, device=None, timeout_s: Optional[float] = None):
         import torch
         import torch.distributed as dist
         self.dist = dist
         self.torch = torch
+        if timeout_s is None:
+            timeout_s = collective_timeout_s()
         if not dist.is_initialized():
             if backend is None:
                 backend = os.environ.get("SERANN_COMM_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
@@ -127,6 +129,14 @@ class TorchDistComm(Comm):
     def shutdown(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+
+def collective_timeout_s() -> float:
+    """Collective timeout: the per-generation job timeout (``worker_pool_job_timeout``, the reference's
+    1080 s pool job timeout) plus a margin for the replicated control plane.  A stalled rank is ended by
+    its own watchdog at the job timeout (utils/faults.py); this bounds how long the others wait."""
+    from ..config import experiment_config
+    return float(experiment_config["worker_pool_job_timeout"]) + 300.0
 
 
 def make_comm(distributed: Optional[bool] = None, backend: Optional[str] = None) -> Comm:

@@ -1,4 +1,4 @@
-"""Fault injection for recovery tests.
+"""Fault injection for recovery tests, and the per-generation watchdog.
 
 The reference delegates failure handling to its external job pool (per-job timeouts, re-dispatch;
 evolutionary_experiment/config.py:7, run_experiment.py:100-108) and has no fault injection.  Here the
@@ -10,16 +10,29 @@ test (or an operator rehearsing a rank loss) kill a rank at a chosen generation:
     SERANN_FAULT_INJECT="generation=2,rank=1"          # only rank 1
     SERANN_FAULT_INJECT="generation=2,rank=1,mode=exit"  # rank 1 exits with status 75 (simulated death)
 
+    SERANN_FAULT_INJECT="generation=2,mode=hang"       # every rank stalls (the watchdog must fire)
+
 The fault fires at the start of the generation, before any training or DB write of it, so the DB
 holds exactly the generations before it.
+
+:class:`GenerationWatchdog` replaces the job pool's per-job timeout (``worker_pool_job_timeout = 1080`` s,
+evolutionary_experiment/config.py:7): a rank whose generation work exceeds it prints the stall and exits
+with status ``EXIT_TIMEOUT`` -- under ``torch.distributed.run`` the other ranks are torn down, and the
+launcher (``cli/launch.py --max-restarts``) relaunches the run with ``--resume-experiment-id``, which
+resumes from the last committed generation.
 """
 from __future__ import annotations
 
 import os
 from typing import Optional
 
+import sys
+import threading
+import time
+
 ENV = "SERANN_FAULT_INJECT"
 EXIT_STATUS = 75
+EXIT_TIMEOUT = 76
 
 
 class InjectedFault(RuntimeError):
@@ -33,12 +46,12 @@ def parse(spec: Optional[str]) -> Optional[dict]:
     for item in spec.split(","):
         key, _, val = item.strip().partition("=")
         if key not in out or not val:
-            raise ValueError(f"{ENV}: bad item {item!r} (expected generation=G[,rank=R][,mode=raise|exit])")
+            raise ValueError(f"{ENV}: bad item {item!r} (expected generation=G[,rank=R][,mode=raise|exit|hang])")
         out[key] = val if key == "mode" else int(val)
     if out["generation"] is None:
         raise ValueError(f"{ENV}: generation=G is required")
-    if out["mode"] not in ("raise", "exit"):
-        raise ValueError(f"{ENV}: mode must be raise or exit")
+    if out["mode"] not in ("raise", "exit", "hang"):
+        raise ValueError(f"{ENV}: mode must be raise, exit or hang")
     return out
 
 
@@ -48,4 +61,49 @@ def maybe_inject(generation: int, rank: int = 0, spec: Optional[str] = None) -> 
         return
     if f["mode"] == "exit":
         os._exit(EXIT_STATUS)
+    if f["mode"] == "hang":
+        while True:                    # a stalled rank: only the watchdog ends this
+            time.sleep(1.0)
     raise InjectedFault(f"injected fault: rank {rank} at generation {generation}")
+
+
+class GenerationWatchdog:
+    """Arms a timer for the work of one generation; if it is not disarmed within ``timeout_s`` the
+    process reports the stall on stderr and exits with ``EXIT_TIMEOUT`` (``os._exit``: a stalled device
+    call or collective cannot be interrupted from Python).  ``timeout_s <= 0`` disables it."""
+
+    def __init__(self, timeout_s: float, rank: int = 0, exit_status: int = EXIT_TIMEOUT):
+        self.timeout_s = float(timeout_s)
+        self.rank = int(rank)
+        self.exit_status = int(exit_status)
+        self._timer: Optional[threading.Timer] = None
+        self._label = ""
+
+    def _fire(self):
+        sys.stderr.write(f"[watchdog] rank {self.rank}: {self._label} exceeded the job timeout of "
+                         f"{self.timeout_s:.0f} s (worker_pool_job_timeout); exiting with status "
+                         f"{self.exit_status} for a relaunch with --resume-experiment-id\n")
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(self.exit_status)
+
+    def arm(self, label: str = "generation") -> "GenerationWatchdog":
+        self.disarm()
+        self._label = label
+        if self.timeout_s > 0:
+            self._timer = threading.Timer(self.timeout_s, self._fire)
+            self._timer.daemon = True
+            self._timer.start()
+        return self
+
+    def disarm(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.disarm()
+        return False
