@@ -3,6 +3,7 @@
 //   train/infer/backward (K05/K06), maxpool fwd/bwd (K03), concat copies (K08), fused heads loss
 //   (softmax-CE + sigmoid-MSE + accuracy + dlogits, K10/K11/K12/K17), popstats (K20-K22).
 // Grouped kernels take a descriptor array and an int2 tile table (problem, chunk).
+#include <hip/hip_fp16.h>
 #include "common.h"
 #include "serann_hip.h"
 
@@ -965,5 +966,40 @@ void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, ui
     if (ntiles <= 0) return;
     hipLaunchKernelGGL(transpose_weights_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
                        as_ptr<const TransDesc>(descs), as_ptr<const int2>(tiles));
+    SERANN_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Replication epilogue (reference experiment_worker.py:151-160, experiment.py:206-209):
+// offspring locus j of a row = round(clip(fp16(sigmoid(z_j)), 0, 1)) -- Keras predicts in fp16, and
+// numpy rounds half to even, so the bit is fp16(sigmoid(z)) > 0.5 (NaN -> 0) -- packed 8 loci per byte,
+// MSB first.  One thread per output byte; grid (row blocks, organisms).
+__global__ __launch_bounds__(256) void rep_bits_kernel(const RepBitsDesc* __restrict__ descs) {
+    const RepBitsDesc& d = descs[blockIdx.y];
+    const int L = (int)d.L, NC = (int)d.NC, nb = (L + 7) >> 3;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;       // byte index
+    if (e >= d.rows * nb) return;
+    const int64_t r = e / nb;
+    const int j0 = (int)(e - r * nb) * 8;
+    const float* z = reinterpret_cast<const float*>(d.logits) + r * (NC + L) + NC;
+    uint32_t byte = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int j = j0 + k;
+        uint32_t bit = 0;
+        if (j < L) {
+            const float s = 1.f / (1.f + expf(-z[j]));
+            bit = __half2float(__float2half_rn(s)) > 0.5f ? 1u : 0u;
+        }
+        byte |= bit << (7 - k);
+    }
+    reinterpret_cast<uint8_t*>(d.out)[e] = (uint8_t)byte;
+}
+
+void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream) {
+    if (ndesc <= 0 || max_rows <= 0) return;
+    const int64_t bytes = max_rows * 32;                 // >= rows * ceil(L / 8) for L <= 256
+    hipLaunchKernelGGL(rep_bits_kernel, dim3((unsigned)((bytes + 255) / 256), (unsigned)ndesc), dim3(256), 0,
+                       as_stream(stream), as_ptr<const RepBitsDesc>(descs));
     SERANN_CHECK(hipGetLastError());
 }

@@ -19,6 +19,7 @@ static py::dict desc_sizes() {
     d["SplitFinDesc"] = sizeof(SplitFinDesc);
     d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
     d["GChainDesc"] = sizeof(GChainDesc);
+    d["RepBitsDesc"] = sizeof(RepBitsDesc);
     return d;
 }
 
@@ -44,6 +45,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("imcol", &launch_imcol);
     m.def("embed_gather", &launch_embed_gather);
     m.def("splitk_finalize", &launch_splitk_finalize);
+    m.def("rep_bits", &launch_rep_bits);
     m.def("concrete_fwd", &launch_concrete_fwd);
     m.def("concrete_bwd", &launch_concrete_bwd);
     m.def("cat_loglik_fwd", &launch_cat_loglik_fwd);

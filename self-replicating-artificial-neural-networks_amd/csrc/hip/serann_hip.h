@@ -101,6 +101,10 @@ struct GChainDesc {
 enum GChainFlags : int64_t { GC_BN = 1, GC_GAMMA = 2, GC_BETA = 4, GC_TRAIN = 8 };
 void launch_gchain(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // single-channel input
+// Replication epilogue (K16): rows [0, rows) of one organism's fp32 head logits [B][NC + L] -> offspring
+// bits, packed MSB-first (numpy.packbits order) into out [rows][ceil(L / 8)] uint8.
+struct RepBitsDesc { int64_t logits, out, rows, NC, L; };
+void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream);
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;
     double lb;

@@ -1073,7 +1073,7 @@ class HipPopulationEngine(PopulationEngine):
                             D = C
                             sl, _ = concat_slices(o, n, F)
                             for q, (pid, col, width, ns, sb) in enumerate(sl):
-                                wg_rows.append(dict(a=dz, b=self._act_ptr(mem, o, pid, inputs), out=gptr(lay.w[n.id]) + 4 * col,
+                                wg_rows.append(dict(a=dz, b=self._act_ptr(mem, o, pid, inputs), out=gptr(lay.w[n.id] + col),
                                                     bias=dbias if q == 0 else 0, aux=yv, act=act, H=Hh, W=1, C=width,
                                                     OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=F, N=width, K=M,
                                                     flags=(H.GF_VEC_A if F % 8 == 0 else 0), ldo=D, _nonarrow=1))
@@ -1585,39 +1585,85 @@ class HipPopulationEngine(PopulationEngine):
         acc, _ = self._evaluate_rows(dd["x"], dd["g"], dd["y"], 0, len(x), cfg)
         return acc
 
-    def replicate(self, genotypes, images, cfg: Optional[TrainConfig] = None) -> List[np.ndarray]:
-        cfg = cfg or self.cfg
-        P = self.num_organisms
-        pool = len(images[0]) if P else 0
-        if pool == 0:
-            return [np.zeros((0, self.layouts[i].ir.genotype_size), np.float32) for i in range(P)]
-        outs = [[] for _ in range(P)]
-        B = min(pool, cfg.batch_size)
-        dev = self.device
-        for c0 in range(0, pool, B):
-            nb = min(B, pool - c0)
-            xs = _padded_zeros((P, B, images[0][0].size), torch.bfloat16, dev)
-            gs = _padded_zeros((P, B, self.layouts[0].ir.genotype_size), torch.bfloat16, dev)
-            xs[:, :nb] = torch.as_tensor(np.stack([im[c0:c0 + nb].reshape(nb, -1) for im in images]),
-                                         dtype=torch.float32, device=dev).to(torch.bfloat16)
-            gs[:, :nb] = torch.as_tensor(np.asarray(genotypes, np.float32), device=dev)[:, None, :].to(torch.bfloat16)
-            mem = self._alloc_buffers(B, with_grads=False) if not hasattr(self, "_rep_mem") or \
-                self._rep_mem["B"] != B else self._rep_mem
-            self._rep_mem = mem
+    def _rep_plan(self, B: int):
+        """Forward-only plan of the replication step at batch B, cached per B: per-organism input
+        buffers (each organism runs on its OWN rows), the inference plan over them,
+        and the fused replication epilogue's descriptors (sigmoid -> fp16 -> round -> bit-pack, K16)."""
+        key = ("rep", B)
+        if key not in self.plans:
+            P, dev = self.num_organisms, self.device
+            n0 = self.layouts[0].ir.nodes[0]
+            xcols = int(math.prod(n0.shape))
+            L = self.layouts[0].ir.genotype_size
+            xs = _padded_zeros((P, B, xcols), torch.bfloat16, dev)
+            gs = _padded_zeros((P, B, L), torch.bfloat16, dev)
             self._input_tensors = getattr(self, "_input_tensors", {})
             for i in range(P):
                 self._input_tensors[xs[i].data_ptr()] = xs[i]
                 self._input_tensors[gs[i].data_ptr()] = gs[i]
+            mem = self._alloc_buffers(B, with_grads=False)
             inputs = [{"X": xs[i].data_ptr(), "g": gs[i].data_ptr()} for i in range(P)]
             plan = self._build_plan("infer", B, mem, inputs)
-            plan.run()
+            nbytes = (L + 7) // 8
+            bits = torch.zeros(P, B, nbytes, dtype=torch.uint8, device=dev)
+            rows = []
             for i, lay in enumerate(self.layouts):
                 ir = lay.ir
-                NC, L = ir.num_classes, ir.genotype_size
                 kind, off = mem["orgs"][i]["act"][ir.cls_head]
-                logits = mem["f32"].view(off, B * (NC + L)).view(B, NC + L)
-                outs[i].append(torch.sigmoid(logits[:nb, NC:]).half().float().cpu().numpy())
-        return [np.concatenate(o, 0) for o in outs]
+                rows.append((mem["f32"].ptr(off), bits[i].data_ptr(), B, ir.num_classes, ir.genotype_size))
+            d = np.array(rows, dtype=H.REPBITS_DTYPE)
+            descs = torch.as_tensor(np.frombuffer(d.tobytes(), dtype=np.uint8).copy(), device=dev)
+            torch.cuda.synchronize(dev)
+            self.plans[key] = dict(plan=plan, xs=xs, gs=gs, mem=mem, bits=bits, descs=descs)
+        return self.plans[key]
+
+    def _replicate_chunks(self, genotypes, images, cfg, packed: bool):
+        cfg = cfg or self.cfg
+        P = self.num_organisms
+        pool = len(images[0]) if P else 0
+        B = min(pool, cfg.batch_size)
+        rp = self._rep_plan(B)
+        dev = self.device
+        L = self.layouts[0].ir.genotype_size
+        g = torch.as_tensor(np.asarray(genotypes, np.float32), device=dev).to(torch.bfloat16)
+        rp["gs"][:] = g[:, None, :]
+        outs = []
+        for c0 in range(0, pool, B):
+            nb = min(B, pool - c0)
+            rp["xs"][:, :nb] = torch.as_tensor(np.stack([im[c0:c0 + nb].reshape(nb, -1) for im in images]),
+                                               dtype=torch.float32, device=dev).to(torch.bfloat16)
+            rp["plan"].run()
+            if packed:
+                self.lib.rep_bits(rp["descs"].data_ptr(), P, B, H.stream_handle())
+                outs.append(rp["bits"][:, :nb].clone())
+            else:
+                mem = rp["mem"]
+                chunk = []
+                for i, lay in enumerate(self.layouts):
+                    ir = lay.ir
+                    NC = ir.num_classes
+                    kind, off = mem["orgs"][i]["act"][ir.cls_head]
+                    logits = mem["f32"].view(off, B * (NC + L)).view(B, NC + L)
+                    chunk.append(torch.sigmoid(logits[:nb, NC:]).half().float())
+                outs.append(torch.stack(chunk))
+        return torch.cat(outs, 1)
+
+    def replicate(self, genotypes, images, cfg: Optional[TrainConfig] = None) -> List[np.ndarray]:
+        """Sigmoid replication outputs (fp16-rounded, as Keras predicts in fp16) per organism."""
+        P = self.num_organisms
+        if P == 0 or len(images[0]) == 0:
+            return [np.zeros((0, self.layouts[i].ir.genotype_size), np.float32) for i in range(P)]
+        out = self._replicate_chunks(genotypes, images, cfg, packed=False).cpu().numpy()
+        return [out[i] for i in range(P)]
+
+    def replicate_packed(self, genotypes, images, cfg: Optional[TrainConfig] = None) -> torch.Tensor:
+        """Offspring genotypes as packed bits straight from the fused epilogue: a device tensor
+        [P][pool][ceil(L / 8)] uint8 (numpy.packbits order) that feeds the all-gather without a host hop."""
+        P = self.num_organisms
+        L = self.layouts[0].ir.genotype_size if P else 0
+        if P == 0 or len(images[0]) == 0:
+            return torch.zeros(P, 0, (L + 7) // 8, dtype=torch.uint8, device=self.device)
+        return self._replicate_chunks(genotypes, images, cfg, packed=True)
 
     def close(self):
         self.graph = None

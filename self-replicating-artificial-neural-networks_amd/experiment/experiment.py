@@ -32,7 +32,7 @@ import numpy as np
 import pandas as pd
 
 from ..genome.interpreter import layer_counts
-from ..parallel.comm import Comm, LocalComm, pack_results, unpack_results
+from ..parallel.comm import Comm, LocalComm, pack_header, unpack_results
 from ..parallel.partition import lpt_partition
 from ..utils.faults import GenerationWatchdog, maybe_inject
 from ..utils.levenshtein import levenshtein_batch
@@ -251,8 +251,11 @@ class Experiment:
                                [plan.results[i].ir for i in local], int(pool_size), generation,
                                self._random_seed, positions=[position[i] for i in local],
                                n_trainable=len(plan.trainable))
-        payload = pack_results(res.indices, res.metrics, res.offspring, res.learning_time, res.replication_time)
-        gathered = comm.allgather_bytes(payload)
+        # one packed all-gather: host header (indices, metrics, timings) + the offspring bits, which stay on
+        # the device from the replication epilogue to the collective (RCCL)
+        head = pack_header(res.indices, res.metrics, int(pool_size), int(p["genotype_size"]), res.learning_time,
+                           res.replication_time)
+        gathered = comm.allgather_payload(head, res.packed)
 
         n = len(current)
         metrics = np.full((n, 4), np.nan)

@@ -54,9 +54,19 @@ def make_engine(name: str, irs: Sequence[OrganismIR], seeds: Sequence[int], devi
 class ShardResult:
     indices: np.ndarray          # (n,) indices into the generation table
     metrics: np.ndarray          # (n, 4): val acc, train acc, test acc, replication mse
-    offspring: np.ndarray        # (n, pool, L) uint8 {0,1} (rounded+clipped replication outputs)
+    packed: object               # (n, pool, ceil(L / 8)) uint8 offspring bits (numpy.packbits order):
+                                 # a device tensor straight from the HIP replication epilogue, or numpy
     learning_time: float
     replication_time: float
+    L: int = 0
+
+    @property
+    def offspring(self) -> np.ndarray:
+        """(n, pool, L) uint8 {0,1} (rounded + clipped replication outputs), unpacked on the host."""
+        p = self.packed
+        if not isinstance(p, np.ndarray):
+            p = p.detach().cpu().numpy()
+        return np.unpackbits(np.asarray(p, np.uint8), axis=-1)[..., :self.L]
 
 
 class ShardWorker:
@@ -84,9 +94,10 @@ class ShardWorker:
         (:mod:`serann.experiment.capacity`); an out-of-memory error splits a wave and retries."""
         n = len(indices)
         L = int(self.params["genotype_size"])
+        nbytes = (L + 7) // 8
         if n == 0:
-            return ShardResult(np.zeros(0, np.int32), np.zeros((0, 4)), np.zeros((0, num_replications, L), np.uint8),
-                               0.0, 0.0)
+            return ShardResult(np.zeros(0, np.int32), np.zeros((0, 4)), np.zeros((0, num_replications, nbytes), np.uint8),
+                               0.0, 0.0, L)
         cfg = self.cfg
         cfg.seed = int(hashlib.blake2b(f"{random_seed}:{generation}:perm".encode(), digest_size=4).hexdigest(), 16)
         seeds = [organism_seed(random_seed, generation, i) for i in ids]
@@ -105,7 +116,7 @@ class ShardWorker:
                      f"(budget {budget / 1e9:.1f} GB)" if budget else f"shard of {n} organisms in {len(waves)} waves")
 
         metrics = np.full((n, 4), np.nan)
-        offspring = np.zeros((n, num_replications, L), np.uint8)
+        packed = None            # device tensor (HIP epilogue) or numpy, [n][pool][nbytes]
         times = [0.0, 0.0]
 
         def run_wave(members: List[int], batch: Optional[int]):
@@ -120,7 +131,11 @@ class ShardWorker:
                     t0 = time.perf_counter()
                     images = [d.test_x[replication_image_rows(pos[i], num_replications, total, len(d.test_x))]
                               for i in members]
-                    outs = engine.replicate(genotypes[members], images, wcfg)
+                    if hasattr(engine, "replicate_packed"):
+                        outs = engine.replicate_packed(genotypes[members], images, wcfg)   # device, packed
+                    else:
+                        outs = np.packbits(np.stack([replication_bits(o) for o in
+                                                     engine.replicate(genotypes[members], images, wcfg)]), axis=-1)
                     rt = time.perf_counter() - t0
             finally:
                 engine.close()
@@ -138,7 +153,11 @@ class ShardWorker:
                 if fit is None:
                     continue                               # did not fit even at half batch: NaN metrics
                 metrics[members] = np.stack([fit.val_acc, fit.train_acc, test_acc, fit.val_mse], axis=1)
-                if outs is not None:
-                    for k, o in zip(members, outs):
-                        offspring[k] = replication_bits(o)
-        return ShardResult(np.asarray(indices, np.int32), metrics.astype(np.float64), offspring, times[0], times[1])
+                if outs is not None and len(members):
+                    if packed is None:
+                        packed = (outs.new_zeros((n, num_replications, nbytes)) if not isinstance(outs, np.ndarray)
+                                  else np.zeros((n, num_replications, nbytes), np.uint8))
+                    packed[members] = outs
+        if packed is None:
+            packed = np.zeros((n, num_replications, nbytes), np.uint8)
+        return ShardResult(np.asarray(indices, np.int32), metrics.astype(np.float64), packed, times[0], times[1], L)

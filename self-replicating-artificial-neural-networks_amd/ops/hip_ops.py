@@ -38,6 +38,7 @@ GCHAIN_DTYPE = np.dtype([(f, _I) for f in ["g", "w1", "b1", "w2", "b2", "y", "dy
                                            "rpb", "dvL1"]] + [("eps", np.float64), ("momentum", np.float64)])
 GC_BN, GC_GAMMA, GC_BETA, GC_TRAIN = 1, 2, 4, 8          # gchain.hip GChainFlags
 GC_FSTAT, GC_FAPPLY, GC_BSTAT, GC_BFULL = 0, 1, 2, 3     # gchain.hip modes
+REPBITS_DTYPE = np.dtype([(f, _I) for f in ["logits", "out", "rows", "NC", "L"]])
 LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target", "metrics", "NC", "L", "B", "flags"]]
                       + [("lb", np.float64)])
 
@@ -248,7 +249,8 @@ def check_layouts():
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("BnDesc", BN_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
-                     ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE)]:
+                     ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
+                     ("RepBitsDesc", REPBITS_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 

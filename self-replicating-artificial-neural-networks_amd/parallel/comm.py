@@ -34,6 +34,12 @@ class Comm:
     def allgather_bytes(self, payload: bytes) -> List[bytes]:
         return [payload]
 
+    def allgather_payload(self, head: bytes, body=None) -> List[bytes]:
+        """All-gather one record per rank made of a small host ``head`` and a ``body`` that may be a
+        device tensor (the packed offspring bits from the replication epilogue): on RCCL the body never
+        visits the host before the collective."""
+        return self.allgather_bytes(head + _host_bytes(body))
+
     def broadcast_bytes(self, payload: Optional[bytes], src: int = 0) -> bytes:
         return payload
 
@@ -96,15 +102,30 @@ class TorchDistComm(Comm):
         return t.to(self.device)
 
     def allgather_bytes(self, payload: bytes) -> List[bytes]:
+        return self._allgather_tensor(self._tensor(payload))
+
+    def allgather_payload(self, head: bytes, body=None) -> List[bytes]:
         torch = self.torch
-        n = torch.tensor([len(payload)], dtype=torch.int64, device=self.device)
+        parts = [self._tensor(head)]
+        if body is not None and len(body):
+            if torch.is_tensor(body):
+                parts.append(body.reshape(-1).to(self.device, torch.uint8))      # device -> device on RCCL
+            else:
+                parts.append(self._tensor(np.ascontiguousarray(body, np.uint8).tobytes()))
+        return self._allgather_tensor(torch.cat(parts) if len(parts) > 1 else parts[0])
+
+    def _allgather_tensor(self, t) -> List[bytes]:
+        """One length exchange + one ``all_gather_into_tensor`` of the records padded to the longest;
+        the gathered buffer comes to the host once, after the collective."""
+        torch = self.torch
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=self.device)
         sizes = [torch.zeros_like(n) for _ in range(self.world_size)]
         self.dist.all_gather(sizes, n)
         sizes = [int(s.item()) for s in sizes]
         mx = max(sizes)
         buf = torch.zeros(mx, dtype=torch.uint8, device=self.device)
-        if payload:
-            buf[:len(payload)] = self._tensor(payload)
+        if t.numel():
+            buf[:t.numel()] = t
         out = torch.empty(self.world_size * mx, dtype=torch.uint8, device=self.device)
         self.dist.all_gather_into_tensor(out, buf)
         host = out.cpu().numpy()
@@ -155,17 +176,37 @@ METRIC_FIELDS = ("classification_validation_accuracy", "classification_training_
                  "classification_test_accuracy", "replication_mse")
 
 
+def _host_bytes(body) -> bytes:
+    if body is None:
+        return b""
+    try:
+        import torch
+        if torch.is_tensor(body):
+            return body.detach().cpu().numpy().astype(np.uint8).tobytes()
+    except ImportError:
+        pass
+    return np.ascontiguousarray(body, np.uint8).tobytes()
+
+
+def pack_header(indices: np.ndarray, metrics: np.ndarray, pool: int, L: int,
+                learning_time: float, replication_time: float) -> bytes:
+    """The host part of a result record: (n, pool, L), the two timings, the organism indices and the
+    (n, 4) float64 metrics.  The packed offspring bits [n][pool][ceil(L / 8)] follow it."""
+    n = len(indices)
+    header = np.array([n, pool if n else 0, L if n else 0], dtype=np.int64).tobytes()
+    times = np.array([learning_time, replication_time], dtype=np.float64).tobytes()
+    return header + times + np.asarray(indices, np.int32).tobytes() + np.asarray(metrics, np.float64).tobytes()
+
+
 def pack_results(indices: np.ndarray, metrics: np.ndarray, offspring: np.ndarray,
                  learning_time: float, replication_time: float) -> bytes:
     """indices: (n,) int32 organism indices in the generation table; metrics: (n, 4) float64;
-    offspring: (n, pool, L) {0,1} -> bit-packed."""
+    offspring: (n, pool, L) {0,1} -> bit-packed (host form of the record)."""
     n = len(indices)
-    header = np.array([n, offspring.shape[1] if n else 0, offspring.shape[2] if n else 0],
-                      dtype=np.int64).tobytes()
-    times = np.array([learning_time, replication_time], dtype=np.float64).tobytes()
-    body = np.asarray(indices, np.int32).tobytes() + np.asarray(metrics, np.float64).tobytes()
+    head = pack_header(indices, metrics, offspring.shape[1] if n else 0, offspring.shape[2] if n else 0,
+                       learning_time, replication_time)
     bits = np.packbits(np.asarray(offspring, np.uint8), axis=-1).tobytes() if n else b""
-    return header + times + body + bits
+    return head + bits
 
 
 def unpack_results(payload: bytes):

@@ -140,8 +140,21 @@ def test_fit_graph_replay_learns():
     acc = eng.evaluate(data.test_x, data.test_labels, data.test_g, cfg)
     assert np.all(acc > 0.2)
     imgs = [data.test_x[:20]] * 3
-    outs = eng.replicate(np.ones((3, 100), np.float32), imgs, cfg)
+    gen = np.random.default_rng(0).integers(0, 2, (3, 100)).astype(np.float32)
+    outs = eng.replicate(gen, imgs, cfg)
     assert outs[0].shape == (20, 100) and np.all((outs[0] >= 0) & (outs[0] <= 1))
+    # the fused replication epilogue (device bit-pack, K16) gives the host rounding of the same outputs
+    from serann.experiment.worker import replication_bits
+    packed = eng.replicate_packed(gen, imgs, cfg)
+    assert packed.shape == (3, 20, 13) and packed.is_cuda
+    bits = np.unpackbits(packed.cpu().numpy(), axis=-1)[..., :100]
+    for i in range(3):
+        assert np.array_equal(bits[i], replication_bits(outs[i])), i
+    # a pool larger than the batch runs in chunks through the same cached plan
+    big = [data.test_x[:700]] * 3
+    pb = eng.replicate_packed(gen, big, TrainConfig(epochs=2, batch_size=300))
+    ob = eng.replicate(gen, big, TrainConfig(epochs=2, batch_size=300))
+    assert np.array_equal(np.unpackbits(pb.cpu().numpy(), axis=-1)[..., :100], np.stack([replication_bits(o) for o in ob]))
 
 
 def test_fit_remainder_batch_matches_torch():
