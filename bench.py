@@ -116,6 +116,12 @@ def main():
                        "global_batch": int(params["training_batch_size"]), "seq_len": int(params["genotype_size"]),
                        "population": pop, "parallelism": f"population-sharded dp{comm.world_size}"},
             "generations": timed,
+            # work normalisation: the evolved population (and so the work of a generation) depends on the
+            # seeded trajectory; model FLOPs of training per generation and the rate achieved on them
+            "train_tflop_per_generation": float(np.mean([h.get("train_tflop", float("nan")) for h in timed]))
+            if timed else None,
+            "achieved_model_tflops": (sum(h.get("train_tflop", 0.0) for h in timed) / elapsed)
+            if elapsed > 0 and timed else None,        # (train_tflop counts the whole population)
         }
         print(json.dumps(out), flush=True)
     if comm.is_root and args.dump_population and db is not None:

@@ -1466,12 +1466,21 @@ class HipPopulationEngine(PopulationEngine):
                 remaining = nfull - 1
             else:
                 remaining = nfull
+            ev = None
+            if graph is not None and remaining > 0 and "replay_ms_per_step" not in self.timings:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             for _ in range(remaining):
                 if graph is not None:
                     graph.replay()
                 else:
                     step()
                 total += 1
+            if ev is not None:
+                # device time per replayed training step of this shard (cost-model calibration, profiling)
+                ev[1].record()
+                ev[1].synchronize()
+                self.timings["replay_ms_per_step"] = ev[0].elapsed_time(ev[1]) / remaining
             if rem_plans is not None and steps > nfull:
                 remainder_step()
                 total += 1

@@ -151,6 +151,7 @@ class Experiment:
             record = dict(generation=generation_number, seconds=None, learning_time=float(np.mean(times["learning_times"] or [0])),
                           replication_time=float(np.mean(times["replication_times"] or [0])),
                           valid=int(len(valid_serann)), population=int(len(current)),
+                          train_tflop=times["train_flops"] / 1e12,
                           mean_val_acc=float(np.nanmean(current["classification_validation_accuracy"]))
                           if len(valid_serann) else float("nan"),
                           stats_db_seconds=t_db - t_stats)
@@ -174,6 +175,9 @@ class Experiment:
             current = next_generation
             record["seconds"] = time.perf_counter() - t0
             record["phases"] = timer.reset()
+            lr = record["phases"].get("learn_and_replicate")
+            if lr:
+                record["achieved_tflops"] = record["train_tflop"] / lr      # model FLOPs / learn+replicate time
             self._print_generation_time(record["seconds"])
             self._finish_record(record, on_generation)
         return self.history
@@ -260,7 +264,7 @@ class Experiment:
         n = len(current)
         metrics = np.full((n, 4), np.nan)
         offspring_rows: Dict[int, np.ndarray] = {}
-        times = {"learning_times": [], "replication_times": []}
+        times = {"learning_times": [], "replication_times": [], "train_flops": self._train_flops(plan)}
         for blob in gathered:
             idx, m, off, lt, rt = unpack_results(blob)
             if len(idx):
@@ -282,6 +286,17 @@ class Experiment:
         # deterministic table order (the reference uses job-completion order)
         offspring_by_id = {ids[i]: offspring_rows[i].astype(np.float64) for i in sorted(offspring_rows)}
         return models_info, offspring_by_id, times
+
+    def _train_flops(self, plan) -> float:
+        """Model FLOPs of this generation's training (forward + backward = 3x the forward FLOPs per
+        sample, over every training row of every epoch, summed over the trainable organisms): the
+        work measure that makes generations with different evolved populations comparable."""
+        cfg = getattr(self._worker, "cfg", None)
+        data = getattr(self._worker, "data", None)
+        if cfg is None or data is None:
+            return float("nan")
+        rows = cfg.split(len(data.train_x)) * int(cfg.epochs)
+        return float(sum(3.0 * plan.results[i].ir.flops_per_sample() for i in plan.trainable) * rows)
 
     # ------------------------------------------------------------------------------------------
     def _select_offspring(self, current: pd.DataFrame, offspring_by_id: Dict[str, np.ndarray]) -> pd.DataFrame:

@@ -8,6 +8,7 @@ from typing import Dict, List, Sequence
 import numpy as np
 
 from ..genome.interpreter import InterpretResult, try_interpret
+from .cost_model import organism_time
 
 
 class InterpretCache:
@@ -61,7 +62,7 @@ class GenerationPlan:
     is_valid: np.ndarray
     is_overweight: np.ndarray
     trainable: np.ndarray          # indices of valid & not overweight organisms
-    costs: np.ndarray              # per trainable organism (training FLOPs per sample)
+    costs: np.ndarray              # per trainable organism: predicted seconds per training step (cost_model)
     arch_keys: List[str]
 
 
@@ -73,6 +74,6 @@ def plan_generation(sources: Sequence[str], cache: InterpretCache, max_parameter
     with np.errstate(invalid="ignore"):
         is_overweight = params > max_parameters          # NaN > x is False, as in the reference
     trainable = np.nonzero(is_valid & ~is_overweight)[0]
-    costs = np.array([results[i].ir.cost_per_sample() + 1e5 for i in trainable], dtype=np.float64)
+    costs = np.array([organism_time(results[i].ir) for i in trainable], dtype=np.float64)
     keys = [results[i].ir.arch_hash() for i in trainable]
     return GenerationPlan(results, is_valid, is_overweight, trainable, costs, keys)
