@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--decode-n", type=int, default=4096)
+    ap.add_argument("--engine", default="auto", choices=["auto", "hip", "torch"],
+                    help="training step: HIP kernels end to end (auto on a GPU) or the torch bf16-autocast path")
     a = ap.parse_args()
     from serann.genome.generator import generate
     from serann.genome.tokenizer import Vocabulary, tokenize
@@ -38,17 +40,18 @@ def main():
     model = ConcreteGAE(100, 350, len(vocab), 50, 2, prior_temperature=0.01)
     quiet = lambda *x, **k: None  # noqa: E731
     train("bench", model, seqs, None, "/tmp/serann_riboae_bench", batch_size=a.batch, min_backup_interval=10 ** 9,
-          max_steps=a.warmup, device=dev, log=quiet, demo_every=0)
+          max_steps=a.warmup, device=dev, log=quiet, demo_every=0, engine=a.engine)
     if dev == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     hist = train("bench", model, seqs, None, "/tmp/serann_riboae_bench", batch_size=a.batch,
-                 min_backup_interval=10 ** 9, max_steps=a.steps, device=dev, log=quiet, demo_every=0)
+                 min_backup_interval=10 ** 9, max_steps=a.steps, device=dev, log=quiet, demo_every=0, engine=a.engine)
     if dev == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"metric": "riboae_train_sequences_per_sec", "value": a.steps * a.batch / dt, "batches_per_sec": a.steps / dt,
-           "ms_per_batch": dt / a.steps * 1e3, "batch": a.batch, "dtype": "bf16 autocast", "loss_first": hist[0],
+           "ms_per_batch": dt / a.steps * 1e3, "batch": a.batch, "engine": a.engine,
+           "dtype": "bf16 operands, fp32 accumulation (HIP kernels)" if a.engine != "torch" else "bf16 autocast", "loss_first": hist[0],
            "loss_last": hist[-1], "device": dev, "params": sum(p.numel() for p in model.parameters())}
     g = np.random.default_rng(0).integers(0, 2, (a.decode_n, 100))
     model.eval()

@@ -233,7 +233,10 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
             const float mu = K + m1;
             const float var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
             mm[c] = mm[c] * mom + mu * (1.f - mom);
-            mv[c] = mv[c] * mom + var * (Rf / (Rf - (1.f + eps))) * (1.f - mom);
+            // BatchNormalizationF16's n / (n - (1 + eps)) (BatchNormalizationF16.py:134-140); flag 64: the
+            // plain Bessel factor n / (n - 1) of a standard BatchNormalization (the RiboAE's)
+            const float ub = (flags & 64) ? Rf / (Rf - 1.f) : Rf / (Rf - (1.f + eps));
+            mv[c] = mv[c] * mom + var * ub * (1.f - mom);
             mean[c] = mu;
             invstd[c] = rsqrtf(var + eps);
         }
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
             float mu, var;
             bn_stats(d, C, Rf, ws, c, mu, var);
-            const float unbiased = var * (Rf / (Rf - (1.f + eps)));
+            const float unbiased = var * ((flags & 64) ? Rf / (Rf - 1.f) : Rf / (Rf - (1.f + eps)));
             mm[c] = mm[c] * mom + mu * (1.f - mom);
             mv[c] = mv[c] * mom + unbiased * (1.f - mom);
             mean[c] = mu;

@@ -6,7 +6,7 @@
 //   s[a]     = logits[a]/t - (1/t) log(-log u[a])                 Gumbel(logits/t, 1/t) sample
 //   logq[a]  = -(zq + e^-zq) + log t,  zq = -log(-log u[a])        posterior log-density
 //   logp[a]  = -(zp + e^-zp) + log tp, zp = (s[a] - log(1/A)/tp) tp prior Gumbel(log(1/A)/tp, 1/tp)
-//   z[a]     = softmax_a(s),   kl[b] += sum_{g,a} logq - logp
+//   z[a]     = softmax_a(s),   kl[b] = sum_{g,a} logq - logp (one block per b, fixed-order sum)
 // (precise logf/expf: -log(-log u) for u near 1 needs log u accurate to relative, not absolute, error)
 // backward (the reparameterised path; logq does not depend on the logits since s - loc = -log(-log u)/t):
 //   dlogits[a] = (1/t) ( z[a] (gz[a] - sum_k z[k] gz[k]) + gkl[b] tp (1 - e^-zp[a]) )
@@ -16,20 +16,28 @@
 //   forward : out[b] = sum_l ( z[b,l,x[b,l]] - logsumexp_v z[b,l,v] )        (model.py:54-59, 45-46)
 //   backward: dz[b,l,v] = g[b] * ( [v == x[b,l]] - softmax_v(z[b,l,:])[v] )
 // z is the generative net's BatchNormalization output [B][L][V] (fp32, V = vocabulary, ~40), x the
-// target tokens [B][L] (int64).  One wave per (b, l-block of 64 positions): each lane owns one position
-// and walks its V logits (two passes: max, then sum-exp and the target logit); the per-sequence sum is
-// a wave reduction + one atomic per wave.  The log-probability tensor [B][L][V] is never materialised.
+// target tokens [B][L] (int64).  One block per sequence b: each lane owns positions l = lane, lane + 256,
+// ... and walks their V logits (two passes: max, then sum-exp and the target logit); the per-sequence sum
+// is a fixed-order block reduction (wave sums, then the 4 waves in order) and a plain store -- no atomics,
+// so the loss is bitwise reproducible.  The log-probability tensor [B][L][V] is never materialised.
+
 #include "common.h"
 #include "serann_hip.h"
 
+// Fixed-order sum of one value per thread over a 256-thread block; thread 0 returns the total.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+    v = warp_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return threadIdx.x == 0 ? ((red[0] + red[1]) + red[2]) + red[3] : 0.f;
+}
+
 __global__ __launch_bounds__(256) void cat_loglik_fwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ x,
                                                              float* __restrict__ out, int B, int L, int V) {
-    const int lanes_per_b = ((L + 63) / 64) * 64;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = (int)(gid / lanes_per_b);
-    const int l = (int)(gid - (int64_t)b * lanes_per_b);
+    __shared__ float red[4];
+    const int b = blockIdx.x;
     float v = 0.f;
-    if (b < B && l < L) {
+    for (int l = threadIdx.x; l < L; l += 256) {
         const float* row = z + ((int64_t)b * L + l) * V;
         float m = -INFINITY;
         for (int k = 0; k < V; ++k) m = fmaxf(m, row[k]);
@@ -37,10 +45,10 @@ __global__ __launch_bounds__(256) void cat_loglik_fwd_kernel(const float* __rest
         for (int k = 0; k < V; ++k) s += __expf(row[k] - m);
         int t = (int)x[(int64_t)b * L + l];
         t = min(max(t, 0), V - 1);
-        v = row[t] - m - __logf(s);
+        v += row[t] - m - __logf(s);
     }
-    v = warp_sum(v);
-    if ((threadIdx.x & 63) == 0 && b < B) atomicAdd(out + b, v);
+    v = block_sum256(v, red);
+    if (threadIdx.x == 0) out[b] = v;
 }
 
 __global__ __launch_bounds__(256) void cat_loglik_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ x,
@@ -82,12 +90,10 @@ __global__ __launch_bounds__(256) void concrete_fwd_kernel(const float* __restri
                                                            float* __restrict__ s_out, float* __restrict__ z_out,
                                                            float* __restrict__ kl, int B, int G, int A, float t, float tp,
                                                            uint32_t k0, uint32_t k1, uint32_t off) {
-    const int lanes_per_b = ((G + 63) / 64) * 64;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = (int)(gid / lanes_per_b);
-    const int g = (int)(gid - (int64_t)b * lanes_per_b);
+    __shared__ float red[4];
+    const int b = blockIdx.x;                    // one block per sequence; loci g = thread, thread + 256, ...
     float klv = 0.f;
-    if (b < B && g < G) {
+    for (int g = threadIdx.x; g < G; g += 256) {
         const int64_t row = (int64_t)b * G + g;
         const float inv_t = 1.f / t, ploc = logf(1.f / (float)A) / tp, log_t = logf(t), log_tp = logf(tp);
         float s[CONCRETE_MAX_A];
@@ -123,8 +129,8 @@ __global__ __launch_bounds__(256) void concrete_fwd_kernel(const float* __restri
             z_out[row * A + a] = expf(s[a] - m) * inv;
         }
     }
-    klv = warp_sum(klv);
-    if ((threadIdx.x & 63) == 0 && b < B) atomicAdd(kl + b, klv);
+    klv = block_sum256(klv, red);
+    if (threadIdx.x == 0) kl[b] = klv;           // fixed-order block sum: no atomics (deterministic)
 }
 
 __global__ __launch_bounds__(256) void concrete_bwd_kernel(const float* __restrict__ s_in, const float* __restrict__ z_in,
@@ -151,8 +157,7 @@ void launch_concrete_fwd(uint64_t logits, uint64_t u, uint64_t s, uint64_t z, ui
                          int64_t A, double t, double tp, uint64_t seed, uint64_t offset, uint64_t stream) {
     if (B <= 0 || G <= 0) return;
     if (A < 1 || A > CONCRETE_MAX_A) throw std::runtime_error("concrete: alphabet size must be in [1, 16]");
-    const int64_t threads = B * (((G + 63) / 64) * 64);
-    hipLaunchKernelGGL(concrete_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(concrete_fwd_kernel, dim3((unsigned)B), dim3(256), 0, as_stream(stream),
                        as_ptr<const float>(logits), as_ptr<const float>(u), as_ptr<float>(s), as_ptr<float>(z),
                        as_ptr<float>(kl), (int)B, (int)G, (int)A, (float)t, (float)tp, (uint32_t)seed,
                        (uint32_t)(seed >> 32), (uint32_t)offset);
@@ -171,8 +176,7 @@ void launch_concrete_bwd(uint64_t s, uint64_t z, uint64_t gz, uint64_t gkl, uint
 // ---- K37 -------------------------------------------------------------------------------------------
 void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream) {
     if (B <= 0 || L <= 0) return;
-    const int64_t threads = B * (((L + 63) / 64) * 64);
-    hipLaunchKernelGGL(cat_loglik_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(cat_loglik_fwd_kernel, dim3((unsigned)B), dim3(256), 0, as_stream(stream),
                        as_ptr<const float>(z), as_ptr<const int64_t>(x), as_ptr<float>(out), (int)B, (int)L, (int)V);
     SERANN_CHECK(hipGetLastError());
 }

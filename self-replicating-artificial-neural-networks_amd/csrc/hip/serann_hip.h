@@ -73,7 +73,8 @@ struct TransDesc { int64_t src, dst, F, P, C; };                             // 
 constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
-    int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx,
+    int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx, 64 moving variance
+                              // with n / (n - 1) (standard BN) instead of BatchNormalizationF16's n / (n - 1 - eps),
                               // bits 4-5 (phase 5): act of the GEMM producing x -- dx is written as that
                               // GEMM's dZ = dx * act'(x) (x is its output), so its backward reads no Y
     double eps, momentum;

@@ -5,7 +5,12 @@ Schedules (per batch number b, clamped to the schedule length):
 * learning rate: logspace(log10(3e-4), log10(2e-5), 1e6)
 * KL weight: linspace(0, 0.2, 1e7) ** 2
 Optimizer: Keras Adam (eps 1e-7) with the scheduled learning rate.  Batches are consumed in dataset
-order with ``repeat()`` semantics (no shuffle), batch 512.  Prints every 10 batches, a reconstruction
+order with ``repeat()`` semantics (no shuffle), batch 512.
+
+Engines: on an MI355X the ConcreteGAE step runs on this repository's HIP kernels end to end
+(:class:`serann.riboae.hip_trainer.HipRiboTrainer`: gemm3 convolutions / Dense, bn_kernel
+BatchNormalization, fused concrete-sample / log-likelihood kernels, the arena Adam; ``engine="hip"``,
+the default on a GPU); ``engine="torch"`` keeps the PyTorch reference path (bf16 autocast on a GPU).  Prints every 10 batches, a reconstruction
 every 50, and keeps only the most recent best-loss checkpoint at least ``min_backup_interval`` batches
 after the previous one -- plus (new) optimizer state + step so training can resume, bf16 autocast on
 MI355X, and an optional ``max_steps`` stop condition (the reference loop is infinite).
@@ -71,26 +76,45 @@ def get_dataset(sequences: np.ndarray, train_test_ratio: float):
 
 def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out_dir: str, batch_size: int = 512,
           min_backup_interval: int = 1000, max_steps: Optional[int] = None, device="cpu", log=print,
-          resume_path: Optional[str] = None, bf16: Optional[bool] = None, demo_every: int = 50, log_every: int = 10):
+          resume_path: Optional[str] = None, bf16: Optional[bool] = None, demo_every: int = 50, log_every: int = 10,
+          engine: str = "auto"):
     dev = torch.device(device)
     model.to(dev).train()
-    opt = ScheduledKerasAdam(list(model.parameters()), lr=learning_rate_at(1), eps=1e-7)
+    is_concrete = isinstance(model, ConcreteGAE)
+    if engine == "auto":
+        engine = "torch"
+        if dev.type == "cuda" and is_concrete and os.environ.get("SERANN_RIBOAE_HIP", "1") != "0":
+            from ..ops.riboae_ops import available
+            if not available():
+                raise RuntimeError("serann_hip extension not loadable on a GPU device (build it, or pass engine='torch')")
+            engine = "hip"
+    hip = None
     start = 1
     min_loss, min_loss_batch = float("inf"), 0
+    ck = None
     if resume_path:
         ck = torch.load(resume_path, map_location=dev, weights_only=True)
         model.load_state_dict(ck["state_dict"])
-        if ck.get("optimizer"):
-            opt.load_state_dict(ck["optimizer"])
         start = int(ck["step"]) + 1
         min_loss = float(ck.get("extra", {}).get("loss", min_loss))
         min_loss_batch = int(ck["step"])
+    if engine == "hip":
+        from .hip_trainer import HipRiboTrainer
+        hip = HipRiboTrainer(model, device=dev, eps=1e-7)      # re-points the parameters into its arenas
+        opt = hip                                               # checkpoints carry its Adam state
+    else:
+        opt = ScheduledKerasAdam(list(model.parameters()), lr=learning_rate_at(1), eps=1e-7)
+    if ck is not None and ck.get("optimizer"):
+        st = ck["optimizer"]
+        if hip is None or "m_arena" in st:
+            opt.load_state_dict(st)
+        else:
+            hip.step_i.fill_(int(st["t"]))                     # a torch-path checkpoint: keep its step count
     if bf16 is None:
         bf16 = dev.type == "cuda"
     data = torch.as_tensor(np.asarray(train_tokens), dtype=torch.long)
     n = len(data)
     nb = max(1, math.ceil(n / batch_size))
-    is_concrete = isinstance(model, ConcreteGAE)
     history = []
     b = start
     t0 = time.perf_counter()
@@ -98,11 +122,14 @@ def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out
         i = (b - 1) % nb
         x = data[i * batch_size:(i + 1) * batch_size].to(dev, non_blocking=True)
         temperature, lr, kw = temperature_at(b), learning_rate_at(b), kld_weight_at(b)
-        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bool(bf16)):
-            metrics = model.compute_loss(x, temperature, kw) if is_concrete else model.compute_loss(x)
-        opt.zero_grad()
-        metrics["loss"].float().backward()
-        opt.step(lr)
+        if hip is not None:
+            metrics = hip.step(x, temperature, kw, lr)
+        else:
+            with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bool(bf16)):
+                metrics = model.compute_loss(x, temperature, kw) if is_concrete else model.compute_loss(x)
+            opt.zero_grad()
+            metrics["loss"].float().backward()
+            opt.step(lr)
         model._param_version = getattr(model, "_param_version", 0) + 1
         loss = float(metrics["loss"].detach())
         history.append(loss)
