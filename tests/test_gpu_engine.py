@@ -76,6 +76,47 @@ def test_train_step_matches_oracle(name):
     assert metrics[0, 3] == 96
 
 
+def _oracle_dev(ir, params, x, g, y, device, dtype):
+    org = Organism(ir, params, device=device, dtype=dtype)
+    xb = torch.as_tensor(x, device=device, dtype=dtype)
+    gb = torch.as_tensor(g, device=device, dtype=dtype)
+    yb = torch.as_tensor(y, device=device)
+    cl, rl = org(xb, gb[..., None], training=True)
+    lb = ir.loss_balance
+    loss = lb * F.cross_entropy(cl.float(), yb) + (1 - lb) * ((torch.sigmoid(rl.float()) - gb.float()) ** 2).mean()
+    loss.backward()
+    grads = {}
+    for k, p in org.params.items():
+        nid, name = k[1:].split("_", 1)
+        grads.setdefault(int(nid), {})[name] = p.grad.detach().float().cpu().numpy()
+    return grads
+
+
+@pytest.mark.parametrize("name", sorted(ARCHS))
+def test_train_step_b750_as_accurate_as_torch_bf16(name):
+    """Production batch (750): every gradient of the HIP engine is within 1.5x (+1 %) of the error that
+    PyTorch's own bf16 computation of the same organism (bf16 weights and activations on the GPU) makes
+    against the fp32 CPU oracle, and the logits within 1 % of the oracle."""
+    from serann.engine.hip_engine import HipPopulationEngine
+    ir = interpret(ARCHS[name])
+    params = init_params(ir, 7)
+    x, g, y = _batch(750, seed=2)
+    eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    grads, metrics = eng.debug_train_step(x, g, y)
+    ref_logits, ref = _oracle(ir, params, x, g, y)
+    assert _rel(eng.debug_logits()[0], ref_logits) < 1e-2
+    bf = _oracle_dev(ir, params, x, g, y, "cuda", torch.bfloat16)
+    hip = eng.export_arena(0, grads)
+    gmax = max(float(np.abs(v).max()) for d in ref.values() for v in d.values())
+    for nid, d in ref.items():
+        for k, v in d.items():
+            if np.linalg.norm(v) < 1e-4 * gmax * np.sqrt(v.size):
+                continue                                   # mathematically ~0: noise in either path
+            e_h, e_b = _rel(hip[nid][k], v), _rel(bf[nid][k], v)
+            assert e_h < 1.5 * e_b + 0.01, (name, nid, k, e_h, e_b)
+    assert metrics[0, 3] == 750
+
+
 def test_population_grouping_matches_single():
     """Grouping heterogeneous organisms into shared launches must not change any organism -- bitwise:
     every reduction split is a function of the organism's own problem (hip_ops: per-problem

@@ -26,39 +26,57 @@ def _batch(B=48, seed=1):
     return x, u
 
 
+SPEC_OF = {"emb": "inference_net.embedding.weight", "c1": "inference_net.conv1.weight",
+           "c1_b": "inference_net.conv1.bias", "c2": "inference_net.conv2.weight", "c3": "inference_net.conv3.weight",
+           "dense": "inference_net.dense.weight", "dense_b": "inference_net.dense.bias",
+           "g1": "generative_net.conv.weight", "g2": "generative_net.dense.weight", "g2_b": "generative_net.dense.bias",
+           "bn0_g": "inference_net.bn0.weight", "bn0_be": "inference_net.bn0.bias", "bn1_g": "inference_net.bn1.weight",
+           "bn3_be": "inference_net.bn3.bias", "gbn1_g": "generative_net.bn1.weight",
+           "gbn2_g": "generative_net.bn2.weight", "gbn2_be": "generative_net.bn2.bias"}
+
+
+def _grads(model, x, u, autocast):
+    out = model.train().compute_loss(x, 0.3, 0.05, noise=u) if not autocast else None
+    if autocast:
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            out = model.train().compute_loss(x, 0.3, 0.05, noise=u)
+    g = torch.autograd.grad(out["loss"].float(), list(model.parameters()))
+    return {n: t.detach().float().cpu().numpy().astype(np.float64) for (n, _), t in zip(model.named_parameters(), g)}, \
+        {k: float(v) for k, v in out.items()}
+
+
+def _err(got, want):
+    err = np.linalg.norm(got - want) / max(np.linalg.norm(want), 1e-30)
+    cos = float(np.dot(got.ravel(), want.ravel()) / max(np.linalg.norm(got) * np.linalg.norm(want), 1e-30))
+    return err, cos
+
+
 def test_hip_step_gradients_match_fp32_oracle(monkeypatch):
+    """Every parameter gradient of one HIP step against the fp32 CPU oracle, judged against PyTorch's own
+    bf16 path on the GPU (autocast): the HIP step must be at least about as accurate.  (Sums that nearly
+    cancel -- a single-channel BatchNorm gamma over 24k elements -- carry bf16 noise in either path.)"""
     from serann.riboae.hip_trainer import HipRiboTrainer
     m = _model()
-    ref = copy.deepcopy(m)                           # CPU fp32 oracle (before the trainer re-points params)
     x, u = _batch()
     monkeypatch.setenv("SERANN_RIBOAE_HIP", "0")
-    out = ref.train().compute_loss(x, 0.3, 0.05, noise=u)
-    names = {id(p): n for n, p in ref.named_parameters()}
-    grads = dict(zip([n for n, _ in ref.named_parameters()],
-                     torch.autograd.grad(out["loss"], list(ref.parameters()))))
+    ref, out = _grads(copy.deepcopy(m), x, u, autocast=False)                      # CPU fp32
+    bf, _ = _grads(copy.deepcopy(m).cuda(), x.cuda(), u.cuda(), autocast=True)     # torch bf16 (GPU)
+    monkeypatch.delenv("SERANN_RIBOAE_HIP")
     m = m.cuda().train()
     tr = HipRiboTrainer(m, device="cuda")
     hip, res = tr.debug_grads(x.cuda(), 0.3, 0.05, u.cuda())
-    assert abs(res["loss"] - float(out["loss"])) < 2e-2 * abs(float(out["loss"])), (res, out)
-    assert abs(res["kld"] - float(out["kld"])) < 2e-2 * abs(float(out["kld"])) + 1e-3
-    spec_of = {"emb": "inference_net.embedding.weight", "c1": "inference_net.conv1.weight",
-               "c1_b": "inference_net.conv1.bias", "c2": "inference_net.conv2.weight", "c3": "inference_net.conv3.weight",
-               "dense": "inference_net.dense.weight", "dense_b": "inference_net.dense.bias",
-               "g1": "generative_net.conv.weight", "g2": "generative_net.dense.weight", "g2_b": "generative_net.dense.bias",
-               "bn0_g": "inference_net.bn0.weight", "bn1_g": "inference_net.bn1.weight",
-               "bn3_be": "inference_net.bn3.bias", "gbn1_g": "generative_net.bn1.weight",
-               "gbn2_g": "generative_net.bn2.weight", "gbn2_be": "generative_net.bn2.bias"}
-    gmax = max(float(g.abs().max()) for g in grads.values())
-    for k, tname in spec_of.items():
-        want = grads[tname].numpy().astype(np.float64)
-        got = hip[k].astype(np.float64)
+    assert abs(res["loss"] - out["loss"]) < 1e-2 * abs(out["loss"]), (res, out)
+    assert abs(res["kld"] - out["kld"]) < 1e-2 * abs(out["kld"]) + 1e-3
+    gmax = max(float(np.abs(g).max()) for g in ref.values())
+    for k, tname in SPEC_OF.items():
+        want, got = ref[tname], hip[k]
         assert got.shape == want.shape, (k, got.shape, want.shape)
         if np.linalg.norm(want) < 1e-4 * gmax * np.sqrt(want.size):
             assert np.abs(got).max() < 1e-2 * gmax, k           # mathematically ~0 (bias before a BN)
             continue
-        err = np.linalg.norm(got - want) / np.linalg.norm(want)
-        cos = float(np.dot(got.ravel(), want.ravel()) / (np.linalg.norm(got) * np.linalg.norm(want)))
-        assert err < 0.05 and cos > 0.998, (k, err, cos)
+        e_h, c_h = _err(got, want)
+        e_b, c_b = _err(bf[tname], want)
+        assert e_h < max(0.03, 1.5 * e_b) and c_h > min(0.9995, c_b - 1e-3), (k, e_h, c_h, e_b, c_b)
 
 
 def test_hip_training_is_bitwise_reproducible():
