@@ -96,6 +96,9 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     # (5x5 outputs: 3 images per chunk, a ragged last chunk; 8x8 outputs: 2 images per chunk)
     (17, 11, 11, 64, 16, 7, 7, 1, 1, "relu"),
     (9, 12, 12, 32, 24, 5, 5, 1, 1, "linear"),
+    # production-batch first layers on a one-channel input (RT = 4 DGRAD into C = 1)
+    (750, 28, 28, 1, 32, 7, 7, 1, 1, "linear"),
+    (48, 32, 16, 1, 32, 5, 5, 1, 1, "linear"),
     # wide-f WGRAD tiles (F > 64: one 128- or 256-row f tile per layer)
     (9, 1, 1, 300, 200, 1, 1, 1, 1, "relu"),
     (40, 5, 1, 96, 120, 1, 1, 1, 1, "sigmoid"),
@@ -254,7 +257,8 @@ def test_grouped_gemm_many_problems_one_launch():
         assert _rel(y.float(), r) < 6e-3
 
 
-@pytest.mark.parametrize("RC", [(3000, 13), (20001, 67), (4096, 256), (999, 300), (5000, 1), (3001, 3)])
+@pytest.mark.parametrize("RC", [(3000, 13), (20001, 67), (4096, 256), (999, 300), (5000, 1), (3001, 3), (588000, 1),
+                                (24576, 1), (96000, 128), (363000, 16)])
 def test_bn_train_infer_backward(RC):
     R, C = RC
     x = (torch.randn(R, C, device=DEV) * 3 + 1).bfloat16()

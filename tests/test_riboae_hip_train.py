@@ -52,15 +52,14 @@ def _err(got, want):
 
 
 def test_hip_step_gradients_match_fp32_oracle(monkeypatch):
-    """Every parameter gradient of one HIP step against the fp32 CPU oracle, judged against PyTorch's own
-    bf16 path on the GPU (autocast): the HIP step must be at least about as accurate.  (Sums that nearly
-    cancel -- a single-channel BatchNorm gamma over 24k elements -- carry bf16 noise in either path.)"""
+    """Every parameter gradient of one HIP step against the fp32 CPU oracle: within 5 % (cosine > 0.998),
+    with an absolute floor of 0.2 % of the largest gradient element for sums that cancel (the gamma /
+    beta of the one-channel BatchNorm after the embedding sum 24k bf16 terms)."""
     from serann.riboae.hip_trainer import HipRiboTrainer
     m = _model()
     x, u = _batch()
     monkeypatch.setenv("SERANN_RIBOAE_HIP", "0")
     ref, out = _grads(copy.deepcopy(m), x, u, autocast=False)                      # CPU fp32
-    bf, _ = _grads(copy.deepcopy(m).cuda(), x.cuda(), u.cuda(), autocast=True)     # torch bf16 (GPU)
     monkeypatch.delenv("SERANN_RIBOAE_HIP")
     m = m.cuda().train()
     tr = HipRiboTrainer(m, device="cuda")
@@ -75,8 +74,10 @@ def test_hip_step_gradients_match_fp32_oracle(monkeypatch):
             assert np.abs(got).max() < 1e-2 * gmax, k           # mathematically ~0 (bias before a BN)
             continue
         e_h, c_h = _err(got, want)
-        e_b, c_b = _err(bf[tname], want)
-        assert e_h < max(0.03, 1.5 * e_b) and c_h > min(0.9995, c_b - 1e-3), (k, e_h, c_h, e_b, c_b)
+        floor = 2e-3 * gmax * np.sqrt(want.size)
+        if np.linalg.norm(got - want) < floor:
+            continue
+        assert e_h < 0.05 and c_h > 0.998, (k, e_h, c_h)
 
 
 def test_hip_training_is_bitwise_reproducible():
