@@ -256,7 +256,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
         p3[j] = (phase == 5) ? sA[256 + ch[j]] : 0.f;
     }
     __syncthreads();
-    const bool reduce = phase == 0 || phase == 4;
+    long long* pdb = reinterpret_cast<long long*>(d.pdb);
+    const bool reduce = phase == 0 || phase == 4 || (phase == 5 && pdb != nullptr);
     if (skip_dx) return;
     float acc0[8], acc1[8];
 #pragma unroll
@@ -293,6 +294,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
                         const float xj = bf2f(cur.xv[k].h[j]);
                         float v = pa[j] * bf2f(cur.gv[k].h[j]) + pb[j] * xj + p3[j] + bf2f(cur.old[k].h[j]);
                         if (pact != ACT_LINEAR) v *= act_grad_from_y(xj, pact);
+                        if (j < nvk) acc0[j] += v;
                         ov.h[j] = f2bf(v);
                     }
                 } else {
@@ -335,8 +337,12 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
             for (int s = t; s < 2048; s += 256) { a += r0[s]; b += r1[s]; }
             for (int o = C; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
             if (lane < C) {
-                fxw_add(wsw + 2 * lane, a);
-                fxw_add(wsw + 2 * (C + lane), b);
+                if (phase == 5) {
+                    fx_add(pdb + lane, a);
+                } else {
+                    fxw_add(wsw + 2 * lane, a);
+                    fxw_add(wsw + 2 * (C + lane), b);
+                }
             }
             return;
         }
@@ -348,8 +354,12 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
                     a += r0[g * 8 * C + c + k * C];
                     b += r1[g * 8 * C + c + k * C];
                 }
-            fxw_add(wsw + 2 * c, a);
-            fxw_add(wsw + 2 * (C + c), b);
+            if (phase == 5) {
+                fx_add(pdb + c, a);
+            } else {
+                fxw_add(wsw + 2 * c, a);
+                fxw_add(wsw + 2 * (C + c), b);
+            }
         }
     }
 }
@@ -450,14 +460,17 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
             const float a = fxw_sum<1>(ws, C, c) / Rf, b = fxw_sum<1>(ws, C, C + c) / Rf;
             const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
             bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
+            float sdz = 0.f;
             for (int r = r0 + rl; r < r1; r += rs) {
                 const int64_t off = (int64_t)r * C + c;
                 const float xh = (bf2f(x[off]) - mu) * is;
                 float v = gg * (bf2f(dy[off]) - a - xh * b);
                 if (flags & 4) v += bf2f(dx[off]);
                 if ((flags >> 4) & 3) v *= act_grad_from_y(bf2f(x[off]), (int)((flags >> 4) & 3));
+                sdz += v;
                 dx[off] = f2bf(v);
             }
+            if (d.pdb) fx_add(reinterpret_cast<long long*>(d.pdb) + c, sdz);   // C > 256: rows of one thread
         }
     }
     if ((phase == 0 || phase == 4) && C <= 256) {

@@ -73,10 +73,15 @@ struct TransDesc { int64_t src, dst, F, P, C; };                             // 
 constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
+    int64_t pdb;              // phase 5: Q32 bias gradient of the GEMM producing x (0 = none), reduced from
+                              // the fp32 dZ before it is rounded to bf16 (serann_hip.h note below)
     int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx, 64 moving variance
                               // with n / (n - 1) (standard BN) instead of BatchNormalizationF16's n / (n - 1 - eps),
                               // bits 4-5 (phase 5): act of the GEMM producing x -- dx is written as that
-                              // GEMM's dZ = dx * act'(x) (x is its output), so its backward reads no Y
+                              // GEMM's dZ = dx * act'(x) (x is its output), so its backward reads no Y.
+                              // pdb: that GEMM's bias gradient sum(dZ) is taken here, in fp32: when the act
+                              // is linear it is mathematically zero (BN removes the mean), and summing the
+                              // bf16-rounded dZ over ~600k rows instead leaves O(sqrt(R) * 2^-9) noise
     double eps, momentum;
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum

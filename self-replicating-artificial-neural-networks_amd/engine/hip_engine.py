@@ -996,7 +996,8 @@ class HipPopulationEngine(PopulationEngine):
 
         # BatchNormalization whose input is the output of an activated GEMM used by nothing else: its
         # backward (phase 5) writes that GEMM's dZ = dx * act'(x) directly, so the GEMM's WGRAD / DGRAD
-        # read dZ alone instead of dY and Y (SERANN_FOLD_BN_ACT=0 turns it off)
+        # read dZ alone instead of dY and Y (SERANN_FOLD_BN_ACT=0 turns it off).  The same BN backward
+        # reduces that GEMM's bias gradient from its fp32 dZ (BnDesc.pdb), so the WGRAD skips it
         dz_folded = [dict() for _ in range(P)]          # gemm id -> act code folded into the BN dx
         if os.environ.get("SERANN_FOLD_BN_ACT", "1") != "0":
             for o, lay in org_iter():
@@ -1014,7 +1015,8 @@ class HipPopulationEngine(PopulationEngine):
                         continue
                     src = ir.node(owner[n.inputs[0]])
                     if (src.op == "gemm" and src.attrs["kind"] not in ("head_cls", "head_rep")
-                            and src.id not in rec["fused_convs"] and src.attrs["act"] in ("relu", "sigmoid")
+                            and src.id not in rec["fused_convs"] and src.id not in rec["gc_nodes"]
+                            and src.attrs["act"] in ("linear", "relu", "sigmoid")
                             and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
                         dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
 
@@ -1062,7 +1064,8 @@ class HipPopulationEngine(PopulationEngine):
                             act = 0 if n.id in dz_folded[o] else H.ACT_CODES[a["act"]]
                         M = B * OH * OW
                         K = KH * KW * C
-                        dbias = gptr(lay.b[n.id]) if n.id in lay.b else 0
+                        # a producer folded into its BN's backward gets its bias gradient from there
+                        dbias = gptr(lay.b[n.id]) if n.id in lay.b and n.id not in dz_folded[o] else 0
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
                         ic = raw_conv_imcol(o, n) if not head else None
@@ -1135,6 +1138,8 @@ class HipPopulationEngine(PopulationEngine):
                         bn_red_cnt.append(H.bn_chunks(R, c, stats=True))
                         if own is not None and own in dz_folded[o]:
                             pflags |= dz_folded[o][own] << 4
+                            if own in lay.b:
+                                base = dict(base, pdb=gptr(lay.b[own]))
                         if own is None:
                             tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
                                                 H.bn_chunks(R, c)))

@@ -21,7 +21,7 @@ GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "
                "ldo"]       # 64-row WGRAD: output row stride (0: N)
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
-                                       "dgamma", "dbeta", "R", "C", "flags"]] + [("eps", np.float64),
+                                       "dgamma", "dbeta", "pdb", "R", "C", "flags"]] + [("eps", np.float64),
                                                                                 ("momentum", np.float64)])
 POOL_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "idx", "dy", "dx", "B", "H", "W", "C", "OH", "OW", "PH", "PW",
                                          "SH", "SW", "flags"]])
