@@ -1,0 +1,42 @@
+"""End-to-end statistical parity of the HIP engine with the fp32 torch engine on generator organisms
+(SURVEY §7.4): 16 organisms drawn from the synthetic generator (genome/generator.py, the reference's
+synthetic_serann_generator), the same initial weights, one epoch on synthetic MNIST at the production
+batch (750).  bf16 operands make the two trajectories diverge step by step, so the test compares what
+the evolution loop consumes -- the per-organism validation accuracy and replication MSE
+(reference experiment_worker.py:66-128) -- not the weights."""
+import numpy as np
+import pytest
+
+from serann.genome.generator import generate
+from serann.genome.interpreter import interpret
+from serann.models.organism import init_params
+
+pytestmark = pytest.mark.gpu
+
+
+def test_generator_population_matches_fp32_torch_engine():
+    import torch
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    from serann.engine.torch_engine import TorchPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=15000, n_test=1000, seed=17),
+                           n_train=15000, n_test=1000)
+    df = generate(16, seed=2024, validation_genotype_size=100)
+    irs = [interpret(code) for code in df["code"]]
+    seeds = list(range(100, 116))
+    cfg = TrainConfig(epochs=1, batch_size=750)
+    hip = HipPopulationEngine(irs, seeds, device="cuda", cfg=cfg,
+                              params=[init_params(ir, s) for ir, s in zip(irs, seeds)])
+    rh = hip.fit(data, cfg)
+    hip.close()
+    ref = TorchPopulationEngine(irs, seeds, device="cuda", compute_dtype=torch.float32, cfg=cfg)
+    rr = ref.fit(data, cfg)
+    assert rh.steps == rr.steps == 19
+    d_acc = np.abs(rh.val_acc - rr.val_acc)
+    r_mse = np.abs(rh.val_mse - rr.val_mse) / np.maximum(rr.val_mse, 1e-6)
+    table = "\n".join(f"{i:2d} acc {a:.4f} vs {b:.4f}  mse {c:.5f} vs {d:.5f}"
+                      for i, (a, b, c, d) in enumerate(zip(rh.val_acc, rr.val_acc, rh.val_mse, rr.val_mse)))
+    assert np.all(np.isfinite(rh.val_acc)) and np.all(np.isfinite(rh.val_mse)), table
+    assert np.all(d_acc <= 0.02), table
+    assert np.all(r_mse <= 0.10), table
