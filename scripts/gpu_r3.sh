@@ -1,25 +1,53 @@
 #!/bin/bash
-# Round-3 GPU session: GPU test tier, then two 1-GPU bench runs whose per-generation records must match
-# (deterministic training), with every GPU step under its own time limit; a failing step stops the script.
-mkdir -p gpurun_out
+# Round-3 GPU session.  STEPS picks the steps (comma list); every GPU step runs under its own time limit and a
+# step that faults, aborts or times out (rc not 0/1) ends the script.
+#   kernels, engine, rest   the GPU test tiers
+#   diag                    per-architecture gradient error report
+#   bench2                  two 1-GPU bench runs whose per-generation records must match (deterministic training)
+#   prof                    rocprofv3 kernel statistics of one bench generation (profiles/r3_kernel_stats.csv)
+#   riboae, riboprof        RiboAE bench on the HIP trainer; rocprofv3 statistics of its training steps
+#   pop1000, calib          the pop-1000 strong-scaling anchor at N=1 (dumps the population); cost-model fit on it
+#   evaluation              seconds per evaluated genotype
+mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
+R=$(pwd)
 run() {
   local name=$1; shift; local to=$1; shift
   echo "=== $name ===" | tee -a gpurun_out/session.log
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "rc=$rc" | tee -a gpurun_out/session.log
-  tail -4 "gpurun_out/$name.log" | tee -a gpurun_out/session.log
+  tail -4 "gpurun_out/$name.log" | cut -c1-600 | tee -a gpurun_out/session.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step $name failed (rc=$rc), stopping"; exit $rc; fi
   return 0
 }
+stats() {   # keep the kernel statistics of a rocprofv3 run, drop the (large) traces
+  local d=$1 out=$2
+  f=$(find "$d" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$out"
+  find "$d" -name "*_trace.csv" -delete
+}
 STEPS=${STEPS:-kernels,engine,rest,diag,bench2}
-[[ $STEPS == *kernels* ]] && run gpukernels 600 python -u -m pytest tests/test_gpu_kernels.py --maxfail=5 -q --timeout 120 --timeout-method thread
-[[ $STEPS == *engine* ]] && run gpuengine 900 python -u -m pytest tests/test_gpu_engine.py --maxfail=5 -v --timeout 300 --timeout-method thread
-[[ $STEPS == *rest* ]] && run gpurest 900 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 300 --timeout-method thread --ignore tests/test_gpu_kernels.py --ignore tests/test_gpu_engine.py
-[[ $STEPS == *diag* ]] && run diag 600 python -u scripts/diag_grad_err.py
-if [[ $STEPS == *bench2* ]]; then
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+has kernels && run gpukernels 600 python -u -m pytest tests/test_gpu_kernels.py --maxfail=5 -q --timeout 120 --timeout-method thread
+has engine && run gpuengine 900 python -u -m pytest tests/test_gpu_engine.py --maxfail=5 -v --timeout 300 --timeout-method thread
+has rest && run gpurest 900 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 400 --timeout-method thread --ignore tests/test_gpu_kernels.py --ignore tests/test_gpu_engine.py
+has diag && run diag 600 python -u scripts/diag_grad_err.py
+if has bench2; then
   run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
   run bench_b 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
 fi
+if has prof; then
+  rm -rf gpurun_out/ev/prof
+  run prof 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ev/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1
+  stats gpurun_out/ev/prof gpurun_out/ev/kernel_stats.csv
+fi
+has riboae && run riboae 400 python scripts/bench_riboae.py --engine hip
+if has riboprof; then
+  rm -rf gpurun_out/ev/riboprof
+  run riboprof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ev/riboprof -o run --output-format csv -- python3 scripts/bench_riboae.py --engine hip --steps 50 --warmup 5 --decode-n 512
+  stats gpurun_out/ev/riboprof gpurun_out/ev/riboae_kernel_stats.csv
+fi
+has pop1000 && run pop1000 1000 python bench.py --gpus 1 --pop-per-gpu 1000 --steps 2 --warmup 1 --dump-population gpurun_out/ev/pop1000.json
+has calib && run calib 900 python scripts/calibrate_cost.py --population-file gpurun_out/ev/pop1000.json --out gpurun_out/ev/cost_model.json
+has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
 exit 0
