@@ -5,6 +5,9 @@ evolutionary_experiment/logic/ribosomal_autoencoder.py:116-124).
   the preceding Conv1D / Dense weights, so decode is two gemm3 MFMA launches (Conv1D 2->32 k5 on the
   LDS-halo implicit-GEMM conv kernel; Dense 3072 -> 350*V on the LDS-tiled kernel with fp32 output) and
   one fused group-argmax launch.  log_softmax is monotone, so it is never materialised.
+  Positions whose top-2 margin lies within the bf16 error bound (~4 % of them on random genotypes) are
+  re-decided in fp32 (``HipRiboDecoder._rescore``), so decode agrees with the fp32 model: a flipped
+  token would be a spurious phenotype mutation in the evolution loop.
 * Training (K37): ``categorical_loglik`` -- log-softmax over the vocabulary, gather at the target
   tokens and the sum over the sequence in one HIP kernel (and its backward), instead of materialising
   the [B][L][V] log-probabilities (model.py:45-46, 54-59).
@@ -52,6 +55,11 @@ class HipRiboDecoder:
             self.b1 = b1.to(self.device, torch.float32).contiguous()
             self.w2 = w2.to(self.device, torch.bfloat16).contiguous()
             self.b2 = b2.to(self.device, torch.float32).contiguous()
+            # fp32 copies for the near-tie rescoring (``_rescore``)
+            self.w1f = (w * s1[:, None, None]).to(self.device, torch.float32).contiguous()   # (32, A, 5)
+            self.b1f = b1.to(self.device, torch.float32).contiguous()
+            self.w2f = w2.to(self.device, torch.float32).contiguous()                      # (L*V, 3072)
+            self.w2n = self.w2f.norm(dim=1).view(L, V).amax(1)                             # (L,)
         self.C1 = w.shape[0]
         self._plans = {}
 
@@ -95,7 +103,46 @@ class HipRiboDecoder:
         for v, d, t in pl["launches"]:
             lib.gemm3(H.MODE_FWD, v, d.data_ptr(), t.data_ptr(), len(t), s)
         lib.group_argmax(pl["logits"].data_ptr(), pl["out"].data_ptr(), B * self.L, self.V, s)
-        return pl["out"].long().clone()
+        out = pl["out"].long().clone()
+        self._rescore(bits, pl, out)
+        return out
+
+    # bf16 operands round each product h_k * w_k by a relative ~2^-9 (input and weight); over the K = 3072
+    # products of a logit that is a random walk of std ~ 2^-9 * sqrt(2/3) * ||h|| ||w|| / sqrt(K).  A position
+    # whose top-2 margin is within TIE_SIGMAS of it (both logits moving) is re-decided in fp32.
+    TIE_SIGMAS = 8.0
+
+    def _rescore(self, bits: torch.Tensor, pl: dict, out: torch.Tensor) -> None:
+        """Re-decide near-tie positions in fp32 so decode matches the fp32 model (the bf16 MFMA path flips
+        ~0.3 % of tokens on random genotypes, each a spurious phenotype mutation in the evolution loop).
+        Flagged positions (usually well under 1 %) get the fp32 conv of their sequence and fp32 dot
+        products for the candidate tokens within the error bound of the top logit."""
+        B, L, V, C1 = out.shape[0], self.L, self.V, self.C1
+        OL = self.G - 4
+        K = OL * C1
+        logits = pl["logits"].view(B, L, V)
+        top = logits.topk(2, dim=-1).values                                   # (B, L, 2)
+        h = pl["h"][:B * K].view(B, K).float()
+        sig = (2.0 ** -9) * (2.0 / 3.0) ** 0.5 * h.norm(dim=1)[:, None] * self.w2n[None, :] / K ** 0.5
+        tau = self.TIE_SIGMAS * 2 ** 0.5 * sig                                # (B, L)
+        flag = (top[..., 0] - top[..., 1]) < tau
+        if not bool(flag.any()):
+            return
+        fb, fl = flag.nonzero(as_tuple=True)
+        ub, inv = torch.unique(fb, return_inverse=True)
+        z = torch.nn.functional.one_hot(bits.to(self.device).long()[ub], self.A).float()     # (nb, G, A)
+        h32 = torch.nn.functional.conv1d(z.permute(0, 2, 1), self.w1f, self.b1f)             # (nb, C1, OL)
+        h32 = h32.permute(0, 2, 1).reshape(len(ub), K)
+        cand = logits[fb, fl] >= (top[fb, fl, 0] - 2 * tau[fb, fl])[:, None]                 # (n, V)
+        ci, cv = cand.nonzero(as_tuple=True)
+        rows = fl[ci] * V + cv
+        vals = torch.empty(len(ci), device=self.device)
+        for c0 in range(0, len(ci), 8192):
+            r = rows[c0:c0 + 8192]
+            vals[c0:c0 + 8192] = (h32[inv[ci[c0:c0 + 8192]]] * self.w2f[r]).sum(1) + self.b2[r]
+        best = torch.full((len(fb), V), float("-inf"), device=self.device)
+        best[ci, cv] = vals
+        out[fb, fl] = best.argmax(1)
 
 
 def _fold_bn(bn):
