@@ -2,7 +2,7 @@
 """Fit the LPT cost model (serann/experiment/cost_model.py) to measured training-step times, and report
 the predicted and measured rank imbalance of the LPT partition.
 
-1. Draw random sub-populations (8..64 organisms) of a population (``--population-file``: JSON sources
+1. Draw random sub-populations (32..160 organisms, around a pop-1000 / 8-rank shard) of a population (``--population-file``: JSON sources
    from ``bench.py --dump-population``, else a generator sample); train each for a few graph-replayed
    steps on the HIP engine and record the device time per step (engine.timings['replay_ms_per_step']).
 2. Fit t = a * sum(3 F B) + b * sum(A B) + c * sum(N) + d by non-negative least squares; print the fit
@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--pop", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--subsets", type=int, default=24)
+    ap.add_argument("--min-size", type=int, default=32, help="sub-population sizes span the shard sizes LPT forms")
+    ap.add_argument("--max-size", type=int, default=160)
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--measure-ranks", type=int, default=0)
     ap.add_argument("--out", default=None)
@@ -78,7 +80,7 @@ def main():
     X, y = [], []
     t0 = time.time()
     for k in range(a.subsets):
-        size = int(rng.integers(8, 65))
+        size = int(rng.integers(a.min_size, a.max_size + 1))
         idx = rng.choice(len(irs), size=min(size, len(irs)), replace=False)
         ms = step_ms([irs[i] for i in idx], data, a.steps)
         X.append(np.concatenate([feats[idx].sum(0), [1.0]]))

@@ -6,6 +6,7 @@
 #   bench2                  two 1-GPU bench runs whose per-generation records must match (deterministic training)
 #   prof                    rocprofv3 kernel statistics of one bench generation (profiles/r3_kernel_stats.csv)
 #   riboae, riboprof        RiboAE bench on the HIP trainer; rocprofv3 statistics of its training steps
+#   popdump, kb             deterministic bench population dump; per-launch step table on it
 #   pop1000, calib          the pop-1000 strong-scaling anchor at N=1 (dumps the population); cost-model fit on it
 #   evaluation              seconds per evaluated genotype
 mkdir -p gpurun_out/ev
@@ -47,7 +48,9 @@ if has riboprof; then
   run riboprof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ev/riboprof -o run --output-format csv -- python3 scripts/bench_riboae.py --engine hip --steps 50 --warmup 5 --decode-n 512
   stats gpurun_out/ev/riboprof gpurun_out/ev/riboae_kernel_stats.csv
 fi
+has popdump && run popdump 600 python bench.py --steps 3 --warmup 1 --dump-population gpurun_out/ev/pop125.json
+has kb && run kb 600 python scripts/bench_kernels.py --population-file gpurun_out/ev/pop125.json --pop 125 --out gpurun_out/ev/kb_pop125.json
 has pop1000 && run pop1000 1000 python bench.py --gpus 1 --pop-per-gpu 1000 --steps 2 --warmup 1 --dump-population gpurun_out/ev/pop1000.json
-has calib && run calib 900 python scripts/calibrate_cost.py --population-file gpurun_out/ev/pop1000.json --out gpurun_out/ev/cost_model.json
+has calib && run calib 900 python scripts/calibrate_cost.py --population-file gpurun_out/ev/pop1000.json --measure-ranks 8 --out gpurun_out/ev/cost_model.json
 has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
 exit 0
