@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--decode-n", type=int, default=4096)
+    ap.add_argument("--train-only", action="store_true",
+                    help="stop after the training measurement (profiling: no torch reference decode / encode)")
     ap.add_argument("--engine", default="auto", choices=["auto", "hip", "torch"],
                     help="training step: HIP kernels end to end (auto on a GPU) or the torch bf16-autocast path")
     a = ap.parse_args()
@@ -53,6 +55,9 @@ def main():
            "ms_per_batch": dt / a.steps * 1e3, "batch": a.batch, "engine": a.engine,
            "dtype": "bf16 operands, fp32 accumulation (HIP kernels)" if a.engine != "torch" else "bf16 autocast", "loss_first": hist[0],
            "loss_last": hist[-1], "device": dev, "params": sum(p.numel() for p in model.parameters())}
+    if a.train_only:
+        print(json.dumps(out))
+        return
     g = np.random.default_rng(0).integers(0, 2, (a.decode_n, 100))
     model.eval()
     ref = model.decode(torch.as_tensor(g, device=dev)).cpu().numpy()

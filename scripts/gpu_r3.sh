@@ -45,7 +45,7 @@ fi
 has riboae && run riboae 400 python scripts/bench_riboae.py --engine hip
 if has riboprof; then
   rm -rf gpurun_out/ev/riboprof
-  run riboprof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ev/riboprof -o run --output-format csv -- python3 scripts/bench_riboae.py --engine hip --steps 50 --warmup 5 --decode-n 512
+  run riboprof 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/ev/riboprof -o run --output-format csv -- python3 scripts/bench_riboae.py --engine hip --steps 50 --warmup 5 --train-only
   stats gpurun_out/ev/riboprof gpurun_out/ev/riboae_kernel_stats.csv
 fi
 has popdump && run popdump 600 python bench.py --steps 3 --warmup 1 --dump-population gpurun_out/ev/pop125.json
