@@ -1155,6 +1155,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
     // GF_BNSTAT: this output feeds a BatchNormalization -- accumulate its phase-0 statistics here
     // (shifted sums against row 0's value, exactly what bn phase 0 would read) into aux[c], aux[N + c]
     const bool bnstat = (d.flags & GF_BNSTAT) != 0;
+    const bool store = (d.flags & GF_NOSTORE) == 0;
     if (!ST && !bnstat && !active) return;
     const int chunk = t % FC, rl = t / FC;
     const int f0 = chunk * 8;
@@ -1229,9 +1230,11 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
             // rows [p0, p1) are one contiguous range; p0 * N * 2 B is a multiple of 16 B
             const int total = (p1 - p0) * N, nvec = total >> 3;
             bf16_t* __restrict__ dst = Y + (int64_t)p0 * N;
-            for (int v = t; v < nvec; v += 256)
-                *reinterpret_cast<uint4*>(dst + 8 * v) = *reinterpret_cast<const uint4*>(&st[8 * v]);
-            for (int e = nvec * 8 + t; e < total; e += 256) dst[e] = st[e];
+            if (store) {
+                for (int v = t; v < nvec; v += 256)
+                    *reinterpret_cast<uint4*>(dst + 8 * v) = *reinterpret_cast<const uint4*>(&st[8 * v]);
+                for (int e = nvec * 8 + t; e < total; e += 256) dst[e] = st[e];
+            }
             __syncthreads();
         }
     } else if (active) {
@@ -1257,7 +1260,8 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                     if (f0 + j < N) stat(j, o.h[j]);
                 }
                 bf16_t* dst = Y + (int64_t)r * N + f0;
-                if (vec) {
+                if (!store) {
+                } else if (vec) {
                     *reinterpret_cast<uint4*>(dst) = o.u4;
                 } else {
 #pragma unroll
@@ -1441,6 +1445,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
     const int t = threadIdx.x, G = 256 / N, q = t / N, i = t - q * N;
     const bool active = q < G;
     const bool bnstat = (d.flags & GF_BNSTAT) != 0;
+    const bool store = (d.flags & GF_NOSTORE) == 0;
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ Wm = reinterpret_cast<const bf16_t*>(d.b);
     const float* bias = reinterpret_cast<const float*>(d.bias);
@@ -1502,7 +1507,8 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
                         s2[j] += dv * dv;
                     }
                 }
-                if (nv == 8) {
+                if (!store) {
+                } else if (nv == 8) {
                     *reinterpret_cast<uint4*>(Y + e) = o.u4;
                 } else {
 #pragma unroll

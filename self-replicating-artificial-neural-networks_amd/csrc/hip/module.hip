@@ -20,6 +20,7 @@ static py::dict desc_sizes() {
     d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
     d["GChainDesc"] = sizeof(GChainDesc);
     d["RepBitsDesc"] = sizeof(RepBitsDesc);
+    d["NbnDesc"] = sizeof(NbnDesc);
     return d;
 }
 
@@ -34,6 +35,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("gather_batch", &launch_gather_batch);
     m.def("counter_add", &launch_counter_add);
     m.def("bn", &launch_bn);
+    m.def("nbn", &launch_nbn);
     m.def("pool", &launch_pool);
     m.def("convpool", &launch_convpool);
     m.def("gchain", &launch_gchain);

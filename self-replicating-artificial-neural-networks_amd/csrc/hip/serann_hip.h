@@ -30,6 +30,8 @@ enum GemmFlags : int64_t {
                           // the splits in order and applies bias + activation (no atomics, no zeroing)
     GF_BNSTAT = 128,      // FWD narrow kernel: also accumulate the consuming BatchNorm's phase-0 statistics
                           // into aux (shifted sums, wide fixed point: the BN statistics workspace format)
+    GF_NOSTORE = 32,      // FWD narrow kernel with GF_BNSTAT: statistics only, the output is never stored
+                          // (its only consumer recomputes it: nbn.hip)
 };
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -110,6 +112,22 @@ struct ImcolDesc { int64_t x, out, B, H, W, OH, OW, KH, KW, SH, SW, K8; };   // 
 // Replication epilogue (K16): rows [0, rows) of one organism's fp32 head logits [B][NC + L] -> offspring
 // bits, packed MSB-first (numpy.packbits order) into out [rows][ceil(L / 8)] uint8.
 struct RepBitsDesc { int64_t logits, out, rows, NC, L; };
+// Fused raw-input Dense (K <= 4 input channels, 8 <= F <= 256 units) -> BatchNormalization, training
+// (nbn.hip).  x: the raw input rows (bf16, row stride ldx); w: bf16 [F][K]; bias fp32 (0 = none); y: the BN
+// output; dy: its gradient; ws / wsb: forward / backward wide statistics workspaces (BnDesc layout);
+// dw, db, dgamma, dbeta: Q32 gradient arena (0 = none); flags as BnDesc (1 gamma, 2 beta, 64 n/(n-1)).
+struct NbnDesc {
+    int64_t x, w, bias, y, dy, gamma, beta, mm, mv, mean, invstd, ws, wsb, dw, db, dgamma, dbeta;
+    int64_t R, F, K, ldx, act, flags;
+    double eps, momentum;
+};
+constexpr int NBN_ELEMS = 16384;       // elements per block of phase 2
+constexpr int NBN_RED_MULT = 4;        // phases 4 / 5 (block reductions) take 4x the rows per block
+__host__ __device__ inline int nbn_super_rows(int F, int phase) {
+    const int s1 = (NBN_ELEMS / 8) / F > 1 ? (NBN_ELEMS / 8) / F : 1;
+    return phase == 2 ? s1 : s1 * NBN_RED_MULT;
+}
+void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream);
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;

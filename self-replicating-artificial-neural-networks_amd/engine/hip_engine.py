@@ -114,6 +114,38 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
     return out
 
 
+FUSE_NBN = os.environ.get("SERANN_FUSE_NBN", "1") != "0"
+
+
+def nbn_pairs(ir: OrganismIR) -> Dict[int, int]:
+    """Raw-input Dense -> BatchNormalization pairs fused in training plans (csrc/hip/nbn.hip): BN id ->
+    Dense id.  Eligible: a Dense with K <= 4 input channels on a raw input (the genotype or the image:
+    no DGRAD), 8 <= units <= 256, whose only consumer is a last-axis BatchNormalization of its units; the
+    Dense then runs as the narrow statistics-only kernel and its output -- and its gradient -- is never
+    materialised in training (SERANN_FUSE_NBN=0 turns it off)."""
+    if not (FUSE_NBN and FUSE_BN_STATS) or "narrow" in H._OFF:
+        return {}
+    consumers: Dict[int, List[int]] = {}
+    for n in ir.nodes:
+        for i in n.inputs:
+            consumers.setdefault(i, []).append(n.id)
+    out = {}
+    for b in ir.nodes:
+        if b.op != "bn" or not b.attrs["last"]:
+            continue
+        n = ir.node(b.inputs[0])
+        if n.op != "gemm" or n.attrs["kind"] != "dense" or ir.cls_head == n.id:
+            continue
+        a = n.attrs
+        if (a["kh"] * a["kw"] != 1 or a["sh"] * a["sw"] != 1 or a["cin"] > 4 or not 8 <= a["f"] <= 256
+                or a["f"] != b.attrs["channels"] or a["act"] not in H.ACT_CODES):
+            continue
+        if ir.node(n.inputs[0]).op != "input" or consumers.get(n.id, []) != [b.id]:
+            continue
+        out[b.id] = n.id
+    return out
+
+
 def _padded_zeros(shape, dtype, device) -> torch.Tensor:
     """Zeroed tensor followed by SLACK zeroed elements (GEMM fragment loads may over-read)."""
     n = math.prod(shape)
@@ -225,6 +257,8 @@ class Plan:
                 L.convpool(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "gchain":
                 L.gchain(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "nbn":
+                L.nbn(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "copy":
                 L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "splitfin":
@@ -770,6 +804,43 @@ class HipPopulationEngine(PopulationEngine):
                     plan.launches.append(Launch("gchain", (mode_, v), desc_tensor(rws, H.GCHAIN_DTYPE), T(tiles),
                                                 len(tiles)))
 
+        # fused raw-input Dense -> BatchNormalization (training): BN id -> Dense id, and the Dense ids
+        nbn = [nbn_pairs(lay.ir) if train and (sel is None or o in sel) else {} for o, lay in enumerate(self.layouts)]
+        nbn_src = [set(m.values()) for m in nbn]
+
+        def nbn_row(o, bid):
+            lay_ = self.layouts[o]
+            rec_ = mem["orgs"][o]
+            ir_ = lay_.ir
+            did = nbn[o][bid]
+            a_ = ir_.node(did).attrs
+            ba = ir_.node(bid).attrs
+            bd = rec_["bn"][bid]
+            bflags = (1 if bid in lay_.gamma else 0) | (2 if bid in lay_.beta else 0)
+            R_ = B * math.prod(ir_.node(bid).shape) // ba["channels"]
+            src_ = ir_.node(ir_.node(did).inputs[0]).attrs["name"]
+            return dict(x=inputs[o][src_], w=wptr_bf(lay_.w[did]), bias=pptr(lay_.b[did]) if did in lay_.b else 0,
+                        y=self._act_ptr(mem, o, bid, inputs),
+                        dy=mem["grad"].ptr(rec_["grad"][bid]) if bid in rec_["grad"] else 0,
+                        gamma=pptr(lay_.gamma[bid]) if bid in lay_.gamma else 0,
+                        beta=pptr(lay_.beta[bid]) if bid in lay_.beta else 0,
+                        mm=sptr(lay_.mm[bid]), mv=sptr(lay_.mv[bid]), mean=f32a.ptr(bd["mean"]),
+                        invstd=f32a.ptr(bd["invstd"]), ws=mem["ws"].ptr(bd["ws"]), wsb=mem["ws"].ptr(bd["wsb"]),
+                        dw=gptr(lay_.w[did]), db=gptr(lay_.b[did]) if did in lay_.b else 0,
+                        dgamma=gptr(lay_.gamma[bid]) if bid in lay_.gamma else 0,
+                        dbeta=gptr(lay_.beta[bid]) if bid in lay_.beta else 0,
+                        R=R_, F=a_["f"], K=a_["cin"], ldx=a_["cin"], act=H.ACT_CODES[a_["act"]], flags=bflags,
+                        eps=ba["epsilon"], momentum=ba["momentum"])
+
+        def add_nbn(rows, phase):
+            by_k: Dict[int, list] = {}
+            for r in rows:
+                by_k.setdefault(int(r["K"]), []).append(r)
+            for k_ in sorted(by_k):
+                rws = by_k[k_]
+                add_chunked("nbn", (phase, k_), rws, H.NBN_DTYPE,
+                            [H.nbn_chunks(r["R"], r["F"], phase) for r in rws], 1)
+
         # gemm node -> the (first) last-axis BatchNormalization reading its output with matching channels
         bn_consumer = [dict() for _ in range(P)]
         bn_prefused = set()
@@ -799,6 +870,7 @@ class HipPopulationEngine(PopulationEngine):
             g_rows, g_dims = [], []
             p_rows, p_cnt = [], []
             bn_rows, bn_cnt, bn_cnt_st, bn_stat = [], [], [], []
+            nbn_rows = []
             c_rows, c_cnt = [], []
             cp_rows = []
             gc_rows = []
@@ -874,6 +946,11 @@ class HipPopulationEngine(PopulationEngine):
                                 g_rows[-1]["aux"] = mem["ws"].ptr(rec["bn"][bnc]["ws"])
                                 g_rows[-1]["flags"] |= H.GF_BNSTAT
                                 bn_prefused.add((o, bnc))
+                                if n.id in nbn_src[o]:
+                                    g_rows[-1]["flags"] |= H.GF_NOSTORE     # recomputed by nbn.hip
+                            elif n.id in nbn_src[o]:
+                                raise RuntimeError(f"organism {o}: Dense {n.id} fused with its BatchNormalization "
+                                                   f"but not on the narrow statistics kernel")
                         if n.id not in fcons[o]:
                             g_dims.append((M, F, K))      # (K slices appended their own dims)
                     elif n.op == "pool":
@@ -882,6 +959,8 @@ class HipPopulationEngine(PopulationEngine):
                                            idx=mem["u8"].ptr(rec["idx"][n.id]), B=B, H=a["h"], W=a["w"], C=a["c"],
                                            OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"]))
                         p_cnt.append(H.pool_units(B * math.prod(n.shape), a["c"]))
+                    elif n.op == "bn" and a["last"] and n.id in nbn[o]:
+                        nbn_rows.append(nbn_row(o, n.id))
                     elif n.op == "bn" and a["last"]:
                         bd = rec["bn"][n.id]
                         c = a["channels"]
@@ -920,6 +999,7 @@ class HipPopulationEngine(PopulationEngine):
             if train:
                 add_gchain([r for r in gc_rows if r["_bn"]], H.GC_FSTAT)
             add_gchain(gc_rows, H.GC_FAPPLY)
+            add_nbn(nbn_rows, 2)
             if bn_rows:
                 if train:
                     need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)
@@ -1026,6 +1106,7 @@ class HipPopulationEngine(PopulationEngine):
             bn_red, bn_red_cnt = [], []
             cpw_rows = []
             gcb_rows = []
+            nbnb_rows = []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             fb = []
             for o, lay in org_iter():
@@ -1041,7 +1122,10 @@ class HipPopulationEngine(PopulationEngine):
                         if n.id in rec["gchain"]:
                             gcb_rows.append(gchain_row(o, n.id))
                         continue
-                    if not rec["req"].get(n.id, False) or n.id in rec["fused_convs"]:
+                    if not rec["req"].get(n.id, False) or n.id in rec["fused_convs"] or n.id in nbn_src[o]:
+                        continue
+                    if n.op == "bn" and n.id in nbn[o]:
+                        nbnb_rows.append(nbn_row(o, n.id))     # BN backward + the Dense's WGRAD (nbn.hip)
                         continue
                     if n.op == "pool" and n.id in cpool[o]:
                         # fused pool backward + conv WGRAD + bias gradient (no DGRAD: raw image input)
@@ -1171,6 +1255,8 @@ class HipPopulationEngine(PopulationEngine):
             add_gchain(gcb_rows, H.GC_BFULL)
             if bn_red:
                 add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
+            add_nbn(nbnb_rows, 4)
+            add_nbn(nbnb_rows, 5)
             for stage in STAGES:
                 batches = [[]]
                 used = [set()]

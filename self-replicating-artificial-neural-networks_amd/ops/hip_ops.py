@@ -43,6 +43,7 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
                       + [("lb", np.float64)])
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 64, 128
+GF_NOSTORE = 32
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -88,6 +89,18 @@ def gemm_desc_array(rows) -> np.ndarray:
 
 
 BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256) BatchNorm kernel
+
+NBN_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "dy", "gamma", "beta", "mm", "mv", "mean", "invstd",
+                                        "ws", "wsb", "dw", "db", "dgamma", "dbeta", "R", "F", "K", "ldx", "act",
+                                        "flags"]] + [("eps", np.float64), ("momentum", np.float64)])
+NBN_ELEMS, NBN_RED_MULT = 16384, 4     # serann_hip.h nbn_super_rows
+
+
+def nbn_chunks(rows: int, units: int, phase: int) -> int:
+    """Blocks of a fused raw-input Dense -> BatchNormalization problem [rows][units] (nbn.hip)."""
+    s1 = max(1, (NBN_ELEMS // 8) // int(units))
+    srb = s1 if phase == 2 else s1 * NBN_RED_MULT
+    return -(-(-(-int(rows) // 8)) // srb)
 
 
 BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block
@@ -250,7 +263,7 @@ def check_layouts():
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
-                     ("RepBitsDesc", REPBITS_DTYPE)]:
+                     ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 

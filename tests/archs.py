@@ -93,6 +93,16 @@ ARCHS = {
         "g_layer = Dense(units=16, activation='relu')(g_layer)\n\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
         "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.7"),
+    # fused raw-input Dense -> BatchNormalization (csrc/hip/nbn.hip): a linear 8-unit image Dense, a
+    # 200-unit sigmoid genotype Dense (one super-row group per block), a Dense after the BN
+    "nbn_wide_linear": (
+        "X_layer = Dense(units=8)(X_layer)\n"
+        "X_layer = BatchNormalization()(X_layer)\n\n"
+        "g_layer = Dense(units=200, activation='sigmoid')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n"
+        "g_layer = Dense(units=10, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.55"),
     # fused genotype chains (csrc/hip/gchain.hip): Conv1D(raw genotype) -> Dense -> [BN] ...
     "gchain_sigmoid_stride2": (
         "X_layer = Dense(units=20, activation='relu')(X_layer)\n"

@@ -335,6 +335,49 @@ def test_gchain_fusion_matches_unfused(name, monkeypatch):
     assert np.allclose(acc_f, acc_p, atol=0.05), (acc_f, acc_p)
 
 
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_wide_linear"])
+def test_nbn_fusion_matches_unfused(name, monkeypatch):
+    """Fused raw-input Dense -> BatchNormalization (nbn.hip: the Dense output is recomputed from the raw
+    input in every pass, dz stays fp32) against the unfused narrow GEMM + BN kernels: logits, every
+    gradient against the fp32 oracle, moving statistics, and inference through the moving statistics."""
+    from serann.engine import hip_engine as he
+    ir = interpret(ARCHS[name])
+    assert he.nbn_pairs(ir), name
+    params = init_params(ir, 5)
+    x, g, y = _batch(96, seed=4)
+    fused = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, mf = fused.debug_train_step(x, g, y)
+    lf = fused.debug_logits()[0]
+    monkeypatch.setattr(he, "FUSE_NBN", False)
+    assert not he.nbn_pairs(ir)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, mp = plain.debug_train_step(x, g, y)
+    lp = plain.debug_logits()[0]
+    ref_logits, ref = _oracle(ir, params, x, g, y)
+    assert _rel(lf, lp) < 1e-2, _rel(lf, lp)
+    assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
+    a, b = fused.export_arena(0, gf), plain.export_arena(0, gp)
+    gmax = max(float(np.abs(v).max()) for d in ref.values() for v in d.values())
+    for nid in ref:
+        for k in ref[nid]:
+            r = np.asarray(ref[nid][k], np.float64)
+            ef, eu = np.linalg.norm(a[nid][k] - r), np.linalg.norm(b[nid][k] - r)
+            floor = 1e-3 * gmax * np.sqrt(r.size)
+            assert ef < 1.25 * eu + 0.02 * np.linalg.norm(r) + floor, (name, nid, k, ef, eu, np.linalg.norm(r))
+    sf, sp = fused.export_params(0), plain.export_params(0)
+    for nid in sp:
+        for k in ("moving_mean", "moving_variance"):
+            if k in sp[nid]:
+                base = np.zeros_like(sp[nid][k]) if k == "moving_mean" else np.ones_like(sp[nid][k])
+                assert _rel(sf[nid][k] - base, sp[nid][k] - base) < 1e-2, (name, nid, k)
+    from serann.engine.base import TrainConfig
+    cfg = TrainConfig(batch_size=48)
+    labels = y.astype(np.int64)
+    acc_f = fused.evaluate(x, labels, g, cfg)
+    acc_p = plain.evaluate(x, labels, g, cfg)
+    assert np.allclose(acc_f, acc_p, atol=0.03), (acc_f, acc_p)
+
+
 def test_adam_kernel_matches_keras_formula():
     from serann.ops import hip_ops as H
     lib = H.lib()

@@ -142,6 +142,30 @@ def test_gchain_eligibility(name, expect):
     assert H.gchain_variant(c.attrs["f"], dn.attrs["f"], c.attrs["kh"]) is not None
 
 
+@pytest.mark.parametrize("name,expect", [
+    ("narrow_bn_ancestor", [75]), ("narrow_bn_x", [24]), ("nbn_wide_linear", [8, 200]),
+    ("odd_channels_bn", []),            # the BN's Dense reads a conv output (needs a DGRAD)
+    ("gchain_sigmoid_stride2", []),     # the BN belongs to the genotype chain's Dense
+    ("empty_x_branch", [])])
+def test_nbn_eligibility(name, expect):
+    """Raw-input Dense (K <= 4) -> BatchNormalization pairs fused in training plans (nbn.hip)."""
+    from serann.engine.hip_engine import nbn_pairs
+    ir = interpret(ARCHS[name])
+    pairs = nbn_pairs(ir)
+    assert sorted(ir.node(d).attrs["f"] for d in pairs.values()) == expect
+    for bid, did in pairs.items():
+        d = ir.node(did)
+        assert ir.node(bid).inputs == [did] and ir.node(d.inputs[0]).op == "input" and d.attrs["cin"] <= 4
+
+
+def test_nbn_chunking_covers_rows():
+    for rows, f in ((75000, 75), (588000, 24), (750 * 100, 200), (17, 8)):
+        for phase in (2, 4, 5):
+            s1 = max(1, (H.NBN_ELEMS // 8) // f)
+            srb = s1 if phase == 2 else s1 * H.NBN_RED_MULT
+            assert H.nbn_chunks(rows, f, phase) * srb * 8 >= rows > (H.nbn_chunks(rows, f, phase) - 1) * srb * 8
+
+
 def test_gchain_variant_and_block_sizing():
     assert H.gchain_variant(32, 51, 5) == 1 * 8 + 2
     assert H.gchain_variant(8, 100, 9) == 1 * 8 + 4
