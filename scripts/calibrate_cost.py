@@ -5,7 +5,8 @@ the predicted and measured rank imbalance of the LPT partition.
 1. Draw random sub-populations (32..160 organisms, around a pop-1000 / 8-rank shard) of a population (``--population-file``: JSON sources
    from ``bench.py --dump-population``, else a generator sample); train each for a few graph-replayed
    steps on the HIP engine and record the device time per step (engine.timings['replay_ms_per_step']).
-2. Fit t = a * sum(3 F B) + b * sum(A B) + c * sum(N) + d by non-negative least squares; print the fit
+2. Fit t = sum_k coef_k * sum(feature_k) + d (cost_model.features: conv / dense FLOPs, BN / other
+   activation elements, nodes) by non-negative least squares; print the fit
    and write the coefficients (``--out``, default the package's parameters/cost_model.json).
 3. Partition the whole population for 2 / 4 / 8 ranks (LPT on the fitted model) and print predicted
    max/mean rank time; with ``--measure-ranks R`` time each of the R shards on this GPU in turn.
@@ -60,7 +61,7 @@ def main():
     ap.add_argument("--population-file", default=None)
     ap.add_argument("--pop", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--subsets", type=int, default=24)
+    ap.add_argument("--subsets", type=int, default=48)
     ap.add_argument("--min-size", type=int, default=32, help="sub-population sizes span the shard sizes LPT forms")
     ap.add_argument("--max-size", type=int, default=160)
     ap.add_argument("--steps", type=int, default=12)
@@ -74,8 +75,12 @@ def main():
     print(f"population: {len(irs)} trainable organisms", flush=True)
     data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=16000, n_test=1000, seed=1),
                            n_train=16000, n_test=1000)
-    feats = np.array([[3.0 * CM.features(ir)["F"] * 750, CM.features(ir)["A"] * 750, CM.features(ir)["N"]]
-                      for ir in irs])
+    names = ["Fc", "Fd", "Ab", "Aa", "N"]
+
+    def row(ir):
+        f = CM.features(ir)
+        return [f[k] * (3.0 * 750 if k.startswith("F") else 750.0) if k in CM.PER_SAMPLE else f[k] for k in names]
+    feats = np.array([row(ir) for ir in irs])
     rng = np.random.default_rng(a.seed)
     X, y = [], []
     t0 = time.time()
@@ -96,8 +101,8 @@ def main():
     pred = X @ coef
     rel = np.abs(pred - y) / y
     r2 = 1 - ((pred - y) ** 2).sum() / ((y - y.mean()) ** 2).sum()
-    out = {"a_s_per_flop": float(coef[0]), "b_s_per_byte": float(coef[1]), "c_s_per_node": float(coef[2]),
-           "d_s": float(coef[3]), "r2": float(r2), "mean_rel_err": float(rel.mean()), "max_rel_err": float(rel.max()),
+    out = {"coef": {k: float(v) for k, v in zip(names, coef[:-1])}, "d_s": float(coef[-1]),
+           "r2": float(r2), "mean_rel_err": float(rel.mean()), "max_rel_err": float(rel.max()),
            "subsets": int(len(y)), "source": "scripts/calibrate_cost.py on one MI355X (graph-replayed steps, B=750)"}
     print(json.dumps(out, indent=1), flush=True)
     if a.out:

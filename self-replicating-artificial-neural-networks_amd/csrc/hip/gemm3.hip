@@ -1180,12 +1180,14 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
             float v = bv[j];
 #pragma unroll
             for (int k = 0; k < K; ++k) v += bf2f(X[k]) * w[j][k];
-            ks[j] = bf2f(f2bf(apply_act(v, act)));
+            ks[j] = store ? bf2f(f2bf(apply_act(v, act))) : apply_act(v, act);
         }
     }
-    auto stat = [&](int j, bf16_t o) {
+    // statistics of what the BN will read: the stored bf16 output, or (GF_NOSTORE: nbn.hip recomputes it)
+    // the fp32 value
+    auto stat = [&](int j, bf16_t o, float yf) {
         if (bnstat) {
-            const float dv = bf2f(o) - ks[j];
+            const float dv = (store ? bf2f(o) : yf) - ks[j];
             s1[j] += dv;
             s2[j] += dv * dv;
         }
@@ -1219,8 +1221,9 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                             float v = bv[j];
 #pragma unroll
                             for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
-                            const bf16_t o = f2bf(apply_act(v, act));
-                            stat(j, o);
+                            const float yf = apply_act(v, act);
+                            const bf16_t o = f2bf(yf);
+                            stat(j, o, yf);
                             st[(r - p0) * N + f0 + j] = o;
                         }
                     }
@@ -1256,8 +1259,9 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_kernel(const GemmDesc* __re
                     float v = bv[j];
 #pragma unroll
                     for (int k = 0; k < K; ++k) v += xv[u][k] * w[j][k];
-                    o.h[j] = f2bf(apply_act(v, act));
-                    if (f0 + j < N) stat(j, o.h[j]);
+                    const float yf = apply_act(v, act);
+                    o.h[j] = f2bf(yf);
+                    if (f0 + j < N) stat(j, o.h[j], yf);
                 }
                 bf16_t* dst = Y + (int64_t)r * N + f0;
                 if (!store) {
@@ -1467,7 +1471,7 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
             float v = bv[j];
 #pragma unroll
             for (int k = 0; k < K; ++k) v += bf2f(X[k]) * w[j][k];
-            ks[j] = bf2f(f2bf(apply_act(v, act)));
+            ks[j] = store ? bf2f(f2bf(apply_act(v, act))) : apply_act(v, act);
         }
     }
     const int64_t total = (int64_t)M * N;
@@ -1500,9 +1504,10 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
                     float v = bv[j];
 #pragma unroll
                     for (int k = 0; k < K; ++k) v += (hi ? xb[u][k] : xa[u][k]) * w[j][k];
-                    o.h[j] = f2bf(apply_act(v, act));
+                    const float yf = apply_act(v, act);
+                    o.h[j] = f2bf(yf);
                     if (bnstat && j < nv) {
-                        const float dv = bf2f(o.h[j]) - ks[j];
+                        const float dv = (store ? bf2f(o.h[j]) : yf) - ks[j];
                         s1[j] += dv;
                         s2[j] += dv * dv;
                     }

@@ -22,6 +22,8 @@
 // partial sums meet in fixed point (common.h fx / fxw): bitwise reproducible in any grouping.
 // Semantics: reference common/BatchNormalizationF16.py:81-153 (unbiased moving variance n / (n - 1 - eps)),
 // Keras Dense (experiment_worker.py:66-128 trains the organism).
+#include <type_traits>
+
 #include "common.h"
 #include "serann_hip.h"
 
@@ -51,13 +53,14 @@ __device__ __forceinline__ NbnCtx nbn_ctx(int F) {
 }
 
 // y of channel f for one raw-input row: exactly the narrow FWD kernel's arithmetic (bias first, then the
-// K products in order, activation, bf16 rounding), so the recomputed value is the one the statistics saw
+// K products in order, activation), so the recomputed value is the one the statistics saw.  The Dense output
+// is never stored, so it is never rounded to bf16 either (the statistics-only FWD pass keeps it fp32 too).
 template <int K>
 __device__ __forceinline__ float nbn_y(const float* xr, const float* w, float b, int act) {
     float v = b;
 #pragma unroll
     for (int k = 0; k < K; ++k) v += xr[k] * w[k];
-    return bf2f(f2bf(apply_act(v, act)));
+    return apply_act(v, act);
 }
 
 }  // namespace
@@ -179,41 +182,54 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
                     }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (nv[u] <= 0) continue;
+            // full super-rows take the unguarded path; only the problem's last super-row can be partial
+            auto body = [&](int u, auto full_tag) {
+                constexpr bool FULL = decltype(full_tag)::value;
                 const int64_t e = (int64_t)(sb + u * c.G) * 8 * F + 8 * c.i;
-                V8 o;
+                float yv[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const bool hi = c.ro[j] != c.ro[0];
-                    const float* xr = hi ? xb[u] : xa[u];
-                    const float y = nbn_y<K>(xr, w[j], bv[j], act);
-                    if (PHASE == 2) {
-                        o.h[j] = f2bf(y * ka[j] + kb[j]);
-                    } else if (j < nv[u]) {
-                        const float gy = bf2f(g[u].h[j]);
-                        if (PHASE == 4) {
-                            acc[j] += gy;
-                            acc[8 + j] += gy * (y - ka[j]) * kb[j];
-                        } else {
-                            float dz = ka[j] * gy + kb[j] * y + kc[j];
-                            if (act != ACT_LINEAR) dz *= act_grad_from_y(y, act);
+                    float xr[K];
 #pragma unroll
-                            for (int k = 0; k < K; ++k) acc[j * K + k] += dz * xr[k];
-                            acc[8 * K + j] += dz;
-                        }
+                    for (int k = 0; k < K; ++k) xr[k] = hi ? xb[u][k] : xa[u][k];
+                    const float y = nbn_y<K>(xr, w[j], bv[j], act);
+                    yv[j] = y;
+                    if (PHASE == 4) {
+                        const float gy = bf2f(g[u].h[j]);              // 0 past the end
+                        acc[j] += gy;
+                        acc[8 + j] += gy * (y - ka[j]) * kb[j];
+                    } else if (PHASE == 5 && (FULL || j < nv[u])) {
+                        const float gy = bf2f(g[u].h[j]);
+                        float dz = ka[j] * gy + kb[j] * y + kc[j];
+                        if (act == ACT_RELU) dz = y > 0.f ? dz : 0.f;
+                        else if (act == ACT_SIGMOID) dz *= y * (1.f - y);
+#pragma unroll
+                        for (int k = 0; k < K; ++k) acc[j * K + k] += dz * xr[k];
+                        acc[8 * K + j] += dz;
                     }
                 }
                 if (PHASE == 2) {
-                    if (nv[u] == 8) {
-                        *reinterpret_cast<uint4*>(Yo + e) = o.u;
+                    uint4 o;
+                    o.x = f2bf2(yv[0] * ka[0] + kb[0], yv[1] * ka[1] + kb[1]);
+                    o.y = f2bf2(yv[2] * ka[2] + kb[2], yv[3] * ka[3] + kb[3]);
+                    o.z = f2bf2(yv[4] * ka[4] + kb[4], yv[5] * ka[5] + kb[5]);
+                    o.w = f2bf2(yv[6] * ka[6] + kb[6], yv[7] * ka[7] + kb[7]);
+                    if (FULL) {
+                        *reinterpret_cast<uint4*>(Yo + e) = o;
                     } else {
+                        V8 ov;
+                        ov.u = o;
 #pragma unroll
                         for (int j = 0; j < 8; ++j)
-                            if (j < nv[u]) Yo[e + j] = o.h[j];
+                            if (j < nv[u]) Yo[e + j] = ov.h[j];
                     }
                 }
+            };
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (nv[u] == 8) body(u, std::true_type{});
+                else if (nv[u] > 0) body(u, std::false_type{});
             }
         }
     }
