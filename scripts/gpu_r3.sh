@@ -51,6 +51,6 @@ fi
 has popdump && run popdump 600 python bench.py --steps 3 --warmup 1 --dump-population gpurun_out/ev/pop125.json
 has kb && run kb 600 python scripts/bench_kernels.py --population-file gpurun_out/ev/pop125.json --pop 125 --out gpurun_out/ev/kb_pop125.json
 has pop1000 && run pop1000 1000 python bench.py --gpus 1 --pop-per-gpu 1000 --steps 2 --warmup 1 --dump-population gpurun_out/ev/pop1000.json
-has calib && run calib 900 python scripts/calibrate_cost.py --population-file gpurun_out/ev/pop1000.json --measure-ranks 8 --out gpurun_out/ev/cost_model.json
+has calib && run calib 900 python scripts/calibrate_cost.py --population-file populations/bench_pop1000_gen2.json --measure-ranks 8 --out gpurun_out/ev/cost_model.json
 has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
 exit 0
