@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--streams", default="4")
+    ap.add_argument("--max-steps", type=int, default=None, help="steps per epoch (profiling runs)")
     ap.add_argument("--ancestor-frac", type=float, default=0.0,
                     help="fraction of the population that are clones of the example.json ancestor (table codec), "
                          "as in the bench's evolved generations")
@@ -57,7 +58,7 @@ def main():
     data = get_serann_data(synthetic_encodings(), synthetic_mnist())
     for ns in a.streams.split(","):
         os.environ["SERANN_STREAMS"] = ns
-        cfg = TrainConfig(epochs=a.epochs, batch_size=750, val_every_epoch=False)
+        cfg = TrainConfig(epochs=a.epochs, batch_size=750, val_every_epoch=False, max_steps_per_epoch=a.max_steps)
         torch.cuda.synchronize()
         ti = time.perf_counter()
         eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
