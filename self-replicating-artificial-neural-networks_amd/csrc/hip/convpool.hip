@@ -96,16 +96,23 @@ struct CpStager {
     }
 };
 
-// Running max of one accumulator element over the window offsets in 2 VALU ops: the window code is
-// packed into the low 8 mantissa bits (255 - code, so that on a tie the first window in (i, j) scan order
-// wins for values >= 0) and the packed values are max-ed as floats.  The kept value is truncated by at
-// most 2^-15 relative before its bf16 rounding.  maxNum drops NaN: a NaN conv output can only come from
-// non-finite filter weights (the image is finite), which are flagged per filter instead (cp_nan).
+// Running max of one accumulator element over the window offsets in a few VALU ops: the window code is
+// packed into the low 8 mantissa bits and the packed values are max-ed as floats.  On a tie the first
+// window in (i, j) scan order wins, as in the reference's MaxPool gradient: for values >= 0 a larger
+// mantissa is larger, so the field holds 255 - code; for negative values (sign bit set) a larger mantissa
+// is smaller, so it holds the code itself.  The kept value is truncated by at most 2^-15 relative before
+// its bf16 rounding.  maxNum drops NaN: a NaN conv output can only come from non-finite filter weights (the
+// image is finite), which are flagged per filter instead (cp_nan).
 __device__ __forceinline__ float cp_key(float v, int code) {
-    return __uint_as_float((__float_as_uint(v) & 0xffffff00u) | (uint32_t)(255 - code));
+    const uint32_t u = __float_as_uint(v);
+    const uint32_t field = (u >> 31) ? (uint32_t)code : (uint32_t)(255 - code);
+    return __uint_as_float((u & 0xffffff00u) | field);
 }
 __device__ __forceinline__ float cp_key_value(float key) { return __uint_as_float(__float_as_uint(key) & 0xffffff00u); }
-__device__ __forceinline__ int cp_key_code(float key) { return 255 - (int)(__float_as_uint(key) & 0xffu); }
+__device__ __forceinline__ int cp_key_code(float key) {
+    const uint32_t u = __float_as_uint(key);
+    return (u >> 31) ? (int)(u & 0xffu) : 255 - (int)(u & 0xffu);
+}
 __device__ __forceinline__ bf16_t cp_bf16(float v) { return __builtin_bit_cast(bf16_t, (__bf16)v); }
 
 // KT: 32-tap k steps; NT: 16-filter tiles per block (<= 4); G: 16-position groups per pass (ILP)

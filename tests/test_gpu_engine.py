@@ -280,6 +280,40 @@ def test_convpool_fusion_matches_unfused(name, monkeypatch):
     assert np.allclose(mf, mp, rtol=2e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+def test_convpool_ties_route_to_the_first_window(sign, monkeypatch):
+    """Pool windows whose conv outputs tie exactly (a centre-tap-only filter on a block-constant image) route
+    the gradient to the first window in scan order -- for negative values too -- as the unfused pool kernel
+    and the reference's MaxPool do; the patches differ off the centre, so the routing shows in dW."""
+    from serann.engine import hip_engine as he
+    src = ("X_layer = Conv2D(filters=16, kernel_size=3, strides=1)(X_layer)\n"
+           "X_layer = MaxPool2D(pool_size=2)(X_layer)\n\n"
+           "g_layer = Dense(units=8, activation='relu')(g_layer)\n\n"
+           "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+           "con = Dense(units=16, activation='relu')(con)\n\nloss_balance = 0.5")
+    ir = interpret(src)
+    cid = next(iter(he.convpool_pairs(ir)))
+    params = init_params(ir, 3)
+    k = np.zeros_like(params[cid]["kernel"])
+    k[1, 1, 0, :] = sign * np.linspace(0.5, 1.0, k.shape[-1])
+    params[cid]["kernel"] = k
+    rng = np.random.default_rng(0)
+    B = 32
+    # conv output position (i, j) reads image pixel (i + 1, j + 1) at the centre tap: make those pixels
+    # constant over every 2 x 2 pool window, and everything else random
+    x = rng.random((B, 28, 28, 1)).astype(np.float32)
+    blocks = rng.random((B, 13, 13)).astype(np.float32) + 0.1
+    x[:, 1:27, 1:27, 0] = np.repeat(np.repeat(blocks, 2, axis=1), 2, axis=2)
+    _, g, y = _batch(B, seed=5)
+    fused = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, _ = fused.debug_train_step(x, g, y)
+    monkeypatch.setattr(he, "FUSE_CONVPOOL", False)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, _ = plain.debug_train_step(x, g, y)
+    a, b = fused.export_arena(0, gf)[cid]["kernel"], plain.export_arena(0, gp)[cid]["kernel"]
+    assert _rel(a, b) < 2e-2, _rel(a, b)
+
+
 @pytest.mark.parametrize("name", [n for n in sorted(ARCHS) if n.startswith("gchain") or n == "convpool_bench_a"])
 def test_gchain_fusion_matches_unfused(name, monkeypatch):
     """Fused genotype chain Conv1D(raw genotype) -> Dense -> [BatchNormalization] (gchain.hip: the chain
