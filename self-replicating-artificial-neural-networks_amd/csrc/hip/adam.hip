@@ -16,14 +16,19 @@ __global__ void adam_scalars_kernel(int* step, float* lr_t, float lr, float b1, 
     *lr_t = lr * sqrtf(1.f - powf(b2, (float)t)) / (1.f - powf(b1, (float)t));
 }
 
+// skip (optional): one byte per 4-parameter group, bit j set = parameter 4i + j was already updated by its
+// WGRAD epilogue (GF_ADAM) this step; fully skipped groups are not even read.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long long* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pbf, const float* __restrict__ lr_t_ptr,
-                                                   int64_t n, float b1, float b2, float eps) {
+                                                   int64_t n, float b1, float b2, float eps,
+                                                   const uint8_t* __restrict__ skip) {
     const float lr_t = *lr_t_ptr;
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const unsigned sk = skip ? skip[i] : 0u;
+        if (sk == 0xfu) continue;
         float4 pv = reinterpret_cast<float4*>(p)[i];
         const longlong2 g01 = reinterpret_cast<longlong2*>(g)[2 * i];
         const longlong2 g23 = reinterpret_cast<longlong2*>(g)[2 * i + 1];
@@ -31,28 +36,36 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long l
         float4 mv = reinterpret_cast<float4*>(m)[i];
         float4 vv = reinterpret_cast<float4*>(v)[i];
         float* pp = &pv.x; float* gg = &gv.x; float* mm = &mv.x; float* vvv = &vv.x;
-        ushort4 ob;
+        ushort4 ob = reinterpret_cast<ushort4*>(pbf)[i];
         uint16_t* o = &ob.x;
+        if (sk == 0u) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
-            vvv[k] = b2 * vvv[k] + (1.f - b2) * gg[k] * gg[k];
-            pp[k] -= lr_t * mm[k] / (sqrtf(vvv[k]) + eps);
-            o[k] = f2bf(pp[k]);
+            for (int k = 0; k < 4; ++k) {
+                adam_elem(pp[k], mm[k], vvv[k], gg[k], lr_t, b1, b2, eps);
+                o[k] = f2bf(pp[k]);
+            }
+            reinterpret_cast<float4*>(p)[i] = pv;
+            reinterpret_cast<float4*>(m)[i] = mv;
+            reinterpret_cast<float4*>(v)[i] = vv;
+            reinterpret_cast<longlong2*>(g)[2 * i] = make_longlong2(0, 0);
+            reinterpret_cast<longlong2*>(g)[2 * i + 1] = make_longlong2(0, 0);
+            reinterpret_cast<ushort4*>(pbf)[i] = ob;
+        } else {
+            // a group straddling a fused tile's edge: element by element
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (sk & (1u << k)) continue;
+                const int64_t e = 4 * i + k;
+                adam_elem(pp[k], mm[k], vvv[k], gg[k], lr_t, b1, b2, eps);
+                p[e] = pp[k]; m[e] = mm[k]; v[e] = vvv[k]; g[e] = 0; pbf[e] = f2bf(pp[k]);
+            }
         }
-        reinterpret_cast<float4*>(p)[i] = pv;
-        reinterpret_cast<float4*>(m)[i] = mv;
-        reinterpret_cast<float4*>(v)[i] = vv;
-        reinterpret_cast<longlong2*>(g)[2 * i] = make_longlong2(0, 0);
-        reinterpret_cast<longlong2*>(g)[2 * i + 1] = make_longlong2(0, 0);
-        reinterpret_cast<ushort4*>(pbf)[i] = ob;
     }
     // tail
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        float gg = fx_f(g[i]);
-        float mm = b1 * m[i] + (1.f - b1) * gg;
-        float vv = b2 * v[i] + (1.f - b2) * gg * gg;
-        float pp = p[i] - lr_t * mm / (sqrtf(vv) + eps);
+        if (skip && ((skip[i >> 2] >> (i & 3)) & 1u)) continue;
+        float pp = p[i], mm = m[i], vv = v[i];
+        adam_elem(pp, mm, vv, fx_f(g[i]), lr_t, b1, b2, eps);
         m[i] = mm; v[i] = vv; p[i] = pp; g[i] = 0; pbf[i] = f2bf(pp);
     }
 }
@@ -62,18 +75,27 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restri
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf(x[i]);
 }
 
-void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
-                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream) {
-    hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(1), 0, s, as_ptr<int>(step), as_ptr<float>(lr_t), lr, b1, b2);
+void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float b2, uint64_t stream) {
+    hipLaunchKernelGGL(adam_scalars_kernel, dim3(1), dim3(1), 0, as_stream(stream), as_ptr<int>(step),
+                       as_ptr<float>(lr_t), lr, b1, b2);
+}
+
+void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
+                        float b1, float b2, float eps, uint64_t skip, uint64_t stream) {
     if (n <= 0) return;
     int64_t blocks = ((n >> 2) + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, as_ptr<float>(p), as_ptr<long long>(g),
-                       as_ptr<float>(m), as_ptr<float>(v), as_ptr<bf16_t>(pbf), as_ptr<const float>(lr_t), n, b1, b2,
-                       eps);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), as_ptr<float>(p),
+                       as_ptr<long long>(g), as_ptr<float>(m), as_ptr<float>(v), as_ptr<bf16_t>(pbf),
+                       as_ptr<const float>(lr_t), n, b1, b2, eps, as_ptr<const uint8_t>(skip));
     SERANN_CHECK(hipGetLastError());
+}
+
+void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
+                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream) {
+    launch_adam_scalars(step, lr_t, lr, b1, b2, stream);
+    launch_adam_update(p, g, m, v, pbf, lr_t, n, b1, b2, eps, 0, stream);
 }
 
 void launch_f32_to_bf16(uint64_t x, uint64_t y, int64_t n, uint64_t stream) {

@@ -100,5 +100,14 @@ __device__ __forceinline__ float fxw_sum(const long long* ws, int C, int idx) {
     return (float)((double)hi + (double)lo * (1.0 / 4294967296.0));
 }
 
+// Keras / TF ResourceApplyAdam on one element (experiment_worker.py:80): shared by the arena-wide Adam pass
+// and the WGRAD epilogues that apply the step to their own tile (GF_ADAM), so both give the same bits.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float lr_t, float b1, float b2,
+                                          float eps) {
+    m = b1 * m + (1.f - b1) * g;
+    v = b2 * v + (1.f - b2) * g * g;
+    p -= lr_t * m / (sqrtf(v) + eps);
+}
+
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename T> static inline T* as_ptr(uint64_t p) { return reinterpret_cast<T*>(p); }

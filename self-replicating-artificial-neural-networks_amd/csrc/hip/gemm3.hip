@@ -731,6 +731,35 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     long long* out = reinterpret_cast<long long*>(d.out);     // Q32 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
+    if ((g.flags & (GF_WSTORE | GF_ADAM)) == (GF_WSTORE | GF_ADAM)) {
+        // sole writer of this tile: apply the optimizer step here (the gradient quantised exactly as the
+        // Q32 arena would hold it) -- the arena-wide Adam pass skips these parameters
+        const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
+        const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
+        float* P = reinterpret_cast<float*>(ac.p);
+        float* Mo = reinterpret_cast<float*>(ac.m);
+        float* Vo = reinterpret_cast<float*>(ac.v);
+        bf16_t* Pb = reinterpret_cast<bf16_t*>(ac.pbf);
+        const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+#pragma unroll
+        for (int i = 0; i < TF; ++i)
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
+                if (col >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
+                    if (row < g.M) {
+                        const int64_t e = e0 + (int64_t)row * ldo + col;
+                        float pv = P[e], mv = Mo[e], vv = Vo[e];
+                        adam_elem(pv, mv, vv, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
+                        P[e] = pv; Mo[e] = mv; Vo[e] = vv; Pb[e] = f2bf(pv);
+                    }
+                }
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < TF; ++i)
 #pragma unroll

@@ -21,6 +21,7 @@ static py::dict desc_sizes() {
     d["GChainDesc"] = sizeof(GChainDesc);
     d["RepBitsDesc"] = sizeof(RepBitsDesc);
     d["NbnDesc"] = sizeof(NbnDesc);
+    d["AdamCtx"] = sizeof(AdamCtx);
     return d;
 }
 
@@ -36,6 +37,8 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("counter_add", &launch_counter_add);
     m.def("bn", &launch_bn);
     m.def("nbn", &launch_nbn);
+    m.def("adam_scalars", &launch_adam_scalars);
+    m.def("adam_update", &launch_adam_update);
     m.def("pool", &launch_pool);
     m.def("convpool", &launch_convpool);
     m.def("gchain", &launch_gchain);

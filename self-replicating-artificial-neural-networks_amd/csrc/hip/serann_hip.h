@@ -18,6 +18,13 @@ struct GemmDesc {
     int64_t ldb;      // LDS-tiled kernel: B row stride (0: K) -- a K slice [.., col0 + K) of a wider [N][ldb] matrix
     int64_t sbase;    // GF_SPLITWS: first workspace slot of this problem (K slices of one output share a workspace)
     int64_t ldo;      // WGRAD (64-row LDS kernel): output row stride (0: N) -- a column slice of a wider dW
+    int64_t adam;     // GF_ADAM: device AdamCtx of the parameter arenas (WGRAD applies Adam to its tile)
+};
+// The parameter / gradient / moment arenas of a population engine (same layout, element e of each is the
+// same parameter) and the device Adam scalars, for WGRAD epilogues that apply the optimizer step (GF_ADAM).
+struct AdamCtx {
+    int64_t p, m, v, pbf, g, lr_t;   // fp32, fp32, fp32, bf16, Q32 int64 arenas; device lr_t (float)
+    float b1, b2, eps, pad;
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
@@ -30,6 +37,8 @@ enum GemmFlags : int64_t {
                           // the splits in order and applies bias + activation (no atomics, no zeroing)
     GF_BNSTAT = 128,      // FWD narrow kernel: also accumulate the consuming BatchNorm's phase-0 statistics
                           // into aux (shifted sums, wide fixed point: the BN statistics workspace format)
+    GF_ADAM = 256,        // WGRAD with GF_WSTORE (sole writer of its tile): apply Keras-Adam to the tile in the
+                          // epilogue instead of storing the gradient; the arena-wide Adam pass skips it
     GF_NOSTORE = 32,      // FWD narrow kernel with GF_BNSTAT: statistics only, the output is never stored
                           // (its only consumer recomputes it: nbn.hip)
 };
@@ -127,6 +136,9 @@ __host__ __device__ inline int nbn_super_rows(int F, int phase) {
     const int s1 = (NBN_ELEMS / 8) / F > 1 ? (NBN_ELEMS / 8) / F : 1;
     return phase == 2 ? s1 : s1 * NBN_RED_MULT;
 }
+void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float b2, uint64_t stream);
+void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
+                        float b1, float b2, float eps, uint64_t skip, uint64_t stream);
 void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream);
 struct LossDesc {

@@ -602,11 +602,16 @@ class HipPopulationEngine(PopulationEngine):
         return [sorted(g) for g in groups if g]
 
     def _build_plan(self, mode: str, B: int, mem, inputs: List[dict], label_ptr: int = 0, target_ptrs=None,
-                    metrics: Optional[torch.Tensor] = None, orgs: Optional[Sequence[int]] = None) -> Plan:
+                    metrics: Optional[torch.Tensor] = None, orgs: Optional[Sequence[int]] = None,
+                    adam_ctx: int = 0) -> Plan:
         """mode in {'train', 'infer'}; inputs[org] = {'X': ptr, 'g': ptr} bf16 device pointers.
-        ``orgs``: build the plan for this subset of organisms only (one plan per stream group)."""
+        ``orgs``: build the plan for this subset of organisms only (one plan per stream group).
+        ``adam_ctx``: device AdamCtx -- WGRAD launches that are the sole writer of their weight tile apply the
+        optimizer step in their epilogue (GF_ADAM; ``plan.adam_regions`` lists those parameters, which the
+        arena-wide Adam pass then skips)."""
         train = mode == "train"
         plan = Plan()
+        plan.adam_regions = []
         P = self.num_organisms
         sel = None if orgs is None else set(int(o) for o in orgs)
 
@@ -648,6 +653,11 @@ class HipPopulationEngine(PopulationEngine):
             for v, rws, tiles in H.gemm3_plan(mode_, rows, dims, splitk=True):
                 if not len(tiles):
                     continue
+                if mode_ == H.MODE_WGRAD:
+                    for r in rws:
+                        if int(r.get("flags", 0)) & H.GF_ADAM:
+                            plan.adam_regions.append(((int(r["out"]) - self.g.data_ptr()) // 8, int(r["M"]),
+                                                      int(r["N"]), int(r.get("ldo") or r["N"])))
                 # split-K FWD problems (merged Dense): fp32 partials per split in a workspace of
                 # the plan, then one grouped finalize launch (ordered sum of splits + bias + activation)
                 fin = []
@@ -1249,7 +1259,6 @@ class HipPopulationEngine(PopulationEngine):
                             col += inner
                     else:
                         fb.append((o, n))
-            add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             add_convpool(cpw_rows, True)
             add_gchain([r for r in gcb_rows if r["_bn"]], H.GC_BSTAT)
             add_gchain(gcb_rows, H.GC_BFULL)
@@ -1283,6 +1292,12 @@ class HipPopulationEngine(PopulationEngine):
                         add_chunked("bn", 5, rows, H.BN_DTYPE, cnts, 1)
                     else:
                         add_chunked("copy", 0, rows, H.COPY_DTYPE, cnts, 1)
+            # WGRAD after this depth's DGRAD: a WGRAD that applies Adam to its tile (GF_ADAM) rewrites the
+            # bf16 weights the layer's DGRAD reads
+            if adam_ctx:
+                for r in wg_rows:
+                    r["adam"] = adam_ctx
+            add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             for o, n in fb:
                 plan.launches.append(Launch("fn", 0, None, None, 0,
                                             self._fallback_bwd(mem, o, n, inputs, B, target, written)))
@@ -1471,7 +1486,22 @@ class HipPopulationEngine(PopulationEngine):
         # so the level-by-level launches of different groups overlap on the GPU (fork/join inside the
         # captured graph).  One group = the single-stream schedule.
         groups = self._stream_groups(int(os.environ.get("SERANN_STREAMS", "4")))
-        plans = [self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics, orgs=g_) for g_ in groups]
+        # WGRAD tiles with a single writer apply Adam in their epilogue (SERANN_FUSE_ADAM=0: the arena pass
+        # does every parameter)
+        actx = np.zeros(1, dtype=H.ADAM_CTX_DTYPE)
+        actx[0] = (self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(), self.g.data_ptr(),
+                   self.lr_t.data_ptr(), cfg.beta1, cfg.beta2, cfg.eps, 0.0)
+        self._adam_ctx = torch.as_tensor(np.frombuffer(actx.tobytes(), dtype=np.uint8).copy(), device=dev)
+        actx_ptr = self._adam_ctx.data_ptr() if os.environ.get("SERANN_FUSE_ADAM", "1") != "0" else 0
+        plans = [self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics, orgs=g_, adam_ctx=actx_ptr)
+                 for g_ in groups]
+
+        def skip_mask(pls):
+            regions = [r for pl in pls for r in pl.adam_regions]
+            if not regions:
+                return None
+            return torch.as_tensor(H.adam_skip_mask(self.p.numel(), regions), device=dev)
+        skip_main = skip_mask(plans)
         if not hasattr(self, "_streams") or len(self._streams) < len(plans):
             self._streams = [torch.cuda.Stream(device=dev) for _ in plans]
         streams = self._streams[:len(plans)]
@@ -1496,16 +1526,20 @@ class HipPopulationEngine(PopulationEngine):
         if Br > 0 and steps > full_steps:
             mem_r = self._alloc_buffers(Br, with_grads=True)
             self._train_mem_rem = mem_r
-            rem_plans = [self._build_plan("train", Br, mem_r, inputs, yb.data_ptr(), targets, metrics, orgs=g_)
-                         for g_ in groups]
+            rem_plans = [self._build_plan("train", Br, mem_r, inputs, yb.data_ptr(), targets, metrics, orgs=g_,
+                                          adam_ctx=actx_ptr) for g_ in groups]
             rem_ws = mem_r["ws"].t
+        skip_rem = skip_mask(rem_plans) if rem_plans is not None else None
+        self._adam_skip = (skip_main, skip_rem)          # referenced by the captured graph
 
-        def step(pls=plans, nb=B, wsb=ws, base=0, ctr=True):
+        def step(pls=plans, nb=B, wsb=ws, base=0, ctr=True, skip=skip_main):
             s = H.stream_handle()
             L.gather_batch(dd["train_x"].data_ptr(), dd["train_g"].data_ptr(), dd["train_y"].data_ptr(),
                            perm_t.data_ptr(), counter.data_ptr() if ctr else 0, base, nb, split, xcols, gcols,
                            xb.data_ptr(), gb.data_ptr(), yb.data_ptr(), s)
             L.memset32(wsb.data_ptr(), 2 * wsb.numel(), s)          # int64 workspace
+            # step counter and lr_t first: the fused WGRAD epilogues read lr_t during the backward
+            L.adam_scalars(self.step_i.data_ptr(), self.lr_t.data_ptr(), cfg.lr, cfg.beta1, cfg.beta2, s)
             if len(pls) == 1:
                 run_plan(pls[0])
             else:
@@ -1518,13 +1552,13 @@ class HipPopulationEngine(PopulationEngine):
                 for st in streams:
                     main.wait_stream(st)
             s = H.stream_handle()
-            L.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
-                   self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), cfg.lr, cfg.beta1, cfg.beta2,
-                   cfg.eps, s)
+            L.adam_update(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                          self.pbf.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), cfg.beta1, cfg.beta2, cfg.eps,
+                          skip.data_ptr() if skip is not None else 0, s)
             L.counter_add(counter.data_ptr(), 1, s)
 
         def remainder_step():
-            step(rem_plans, Br, rem_ws, full_steps * B, False)
+            step(rem_plans, Br, rem_ws, full_steps * B, False, skip_rem)
 
         use_graph = full_steps > 1
         graph = None

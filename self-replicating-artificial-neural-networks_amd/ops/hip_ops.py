@@ -18,7 +18,8 @@ GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "
                "kper",      # GF_SPLITWS: k steps per split
                "ldb",       # LDS-tiled kernel: B row stride (0: K)
                "sbase",     # GF_SPLITWS: first workspace slot
-               "ldo"]       # 64-row WGRAD: output row stride (0: N)
+               "ldo",       # 64-row WGRAD: output row stride (0: N)
+               "adam"]      # GF_ADAM: device AdamCtx
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
                                        "dgamma", "dbeta", "pdb", "R", "C", "flags"]] + [("eps", np.float64),
@@ -44,6 +45,8 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 64, 128
 GF_NOSTORE = 32
+GF_ADAM = 256
+ADAM_CTX_DTYPE = np.dtype([(f, _I) for f in ['p', 'm', 'v', 'pbf', 'g', 'lr_t']] + [(f, np.float32) for f in ['b1', 'b2', 'eps', 'pad']])
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -126,6 +129,24 @@ def to_q32(t):
 def from_q32(t) -> np.ndarray:
     """int64 Q32 tensor -> float64 numpy array."""
     return t.detach().cpu().numpy().astype(np.float64) / Q32
+
+
+def adam_skip_mask(n: int, regions) -> np.ndarray:
+    """Skip mask of the arena-wide Adam pass (adam.hip): one uint8 per 4-parameter group (plus the tail
+    group), bit j = parameter 4i + j is updated by its WGRAD epilogue (GF_ADAM).  ``regions``: (first
+    element, rows, cols, row stride) blocks of the parameter arena."""
+    fused = np.zeros(((int(n) + 3) // 4) * 4, dtype=bool)
+    for off, rows, cols, ld in regions:
+        off, rows, cols, ld = int(off), int(rows), int(cols), int(ld)
+        if rows <= 0 or cols <= 0:
+            continue
+        if ld == cols:
+            fused[off:off + rows * cols] = True
+        else:
+            idx = off + np.arange(rows)[:, None] * ld + np.arange(cols)[None, :]
+            fused[idx.ravel()] = True
+    b = fused.reshape(-1, 4).astype(np.uint8)
+    return (b[:, 0] | (b[:, 1] << 1) | (b[:, 2] << 2) | (b[:, 3] << 3)).astype(np.uint8)
 
 
 def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
@@ -263,7 +284,7 @@ def check_layouts():
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
-                     ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE)]:
+                     ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE), ("AdamCtx", ADAM_CTX_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
@@ -559,6 +580,10 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
+                        if r.get("adam"):
+                            r["flags"] |= GF_ADAM      # sole writer: apply the optimizer step in the epilogue
+                    else:
+                        r["adam"] = 0
             elif mode == MODE_FWD and 7000 < v < 7300:
                 tl = []
                 for p, (r, (M, N, K)) in enumerate(items):

@@ -172,6 +172,32 @@ def test_fit_is_bitwise_reproducible():
     assert np.array_equal(r0.val_mse, r1.val_mse)
 
 
+def test_fused_adam_matches_the_arena_pass(monkeypatch):
+    """WGRAD tiles with a single writer apply Adam in their epilogue (GF_ADAM) and the arena-wide pass skips
+    them: after a 2-epoch fit (graph replay, remainder step) weights, moments and bf16 copies are bitwise
+    those of the arena pass over every parameter."""
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=2200, n_test=300, seed=8),
+                           n_train=2200, n_test=300)
+    names = sorted(ARCHS)
+    irs = [interpret(ARCHS[n]) for n in names]
+    cfg = TrainConfig(epochs=2, batch_size=256)
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SERANN_FUSE_ADAM", fuse)
+        eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
+        res = eng.fit(data, cfg)
+        out.append((eng.p.cpu(), eng.m.cpu(), eng.v.cpu(), eng.pbf.cpu(), res, eng._adam_skip))
+        del eng
+    (p1, m1, v1, b1, r1, sk1), (p0, m0, v0, b0, r0, sk0) = out
+    assert sk1[0] is not None and int((sk1[0] != 0).sum()) > 0       # some tiles were fused
+    assert sk0[0] is None
+    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0) and torch.equal(b1, b0)
+    assert np.array_equal(r1.val_acc, r0.val_acc)
+
+
 def test_fit_graph_replay_learns():
     from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
     from serann.engine.base import TrainConfig

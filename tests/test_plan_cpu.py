@@ -197,3 +197,16 @@ def test_conv_wgrad_multi_image_chunks():
     (v, rws, tiles), = H.gemm3_plan(H.MODE_WGRAD, rows, [(16, 3136, 17 * 25)])
     assert v >= 3000000
     assert int(tiles[:, 3].max()) == 6 and int(tiles[:, 2].min()) == 0      # ceil(17 / 3) chunks
+
+
+def test_adam_skip_mask():
+    """One byte per 4-parameter group of the arena-wide Adam pass; bit j = parameter 4i + j is updated by its
+    WGRAD epilogue.  Regions are strided blocks (a column slice of a merged Dense's weights)."""
+    n = 50
+    m = H.adam_skip_mask(n, [(3, 2, 3, 10), (40, 1, 6, 6)])
+    assert m.dtype == np.uint8 and len(m) == -(-n // 4)
+    want = np.zeros(52, bool)
+    for e in (3, 4, 5, 13, 14, 15, 40, 41, 42, 43, 44, 45):
+        want[e] = True
+    bits = np.unpackbits(m[:, None], axis=1, bitorder="little")[:, :4].ravel().astype(bool)
+    assert np.array_equal(bits, want)
