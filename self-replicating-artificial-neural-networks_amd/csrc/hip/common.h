@@ -102,11 +102,15 @@ __device__ __forceinline__ float fxw_sum(const long long* ws, int C, int idx) {
 
 // Keras / TF ResourceApplyAdam on one element (experiment_worker.py:80): shared by the arena-wide Adam pass
 // and the WGRAD epilogues that apply the step to their own tile (GF_ADAM), so both give the same bits.
+// Every operation is spelled out (explicit fma, IEEE sqrt and division, no contraction) so the two call
+// sites cannot be compiled into different roundings.
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float lr_t, float b1, float b2,
                                           float eps) {
-    m = b1 * m + (1.f - b1) * g;
-    v = b2 * v + (1.f - b2) * g * g;
-    p -= lr_t * m / (sqrtf(v) + eps);
+#pragma clang fp contract(off)
+    m = __fmaf_rn(b1, m, (1.f - b1) * g);
+    v = __fmaf_rn(b2, v, ((1.f - b2) * g) * g);
+    const float den = __fsqrt_rn(v) + eps;
+    p = p - __fdiv_rn(lr_t * m, den);
 }
 
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }

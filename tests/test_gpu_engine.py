@@ -194,7 +194,8 @@ def test_fused_adam_matches_the_arena_pass(monkeypatch):
     (p1, m1, v1, b1, r1, sk1), (p0, m0, v0, b0, r0, sk0) = out
     assert sk1[0] is not None and int((sk1[0] != 0).sum()) > 0       # some tiles were fused
     assert sk0[0] is None
-    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0) and torch.equal(b1, b0)
+    diffs = {k: float((a - b).abs().max()) for k, a, b in (("p", p1, p0), ("m", m1, m0), ("v", v1, v0))}
+    assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0) and torch.equal(b1, b0), diffs
     assert np.array_equal(r1.val_acc, r0.val_acc)
 
 
