@@ -8,6 +8,8 @@
 #   riboae, riboprof        RiboAE bench on the HIP trainer; rocprofv3 statistics of its training steps
 #   popdump, kb             deterministic bench population dump; per-launch step table on it
 #   pop1000, calib          the pop-1000 strong-scaling anchor at N=1 (dumps the population); cost-model fit on it
+#   bench1                  one 1-GPU bench run
+#   pop50                   BASELINE config #2: pop 50, example.json, 1 GPU
 #   evaluation              seconds per evaluated genotype
 mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
@@ -52,5 +54,7 @@ has popdump && run popdump 600 python bench.py --steps 3 --warmup 1 --dump-popul
 has kb && run kb 600 python scripts/bench_kernels.py --population-file gpurun_out/ev/pop125.json --pop 125 --out gpurun_out/ev/kb_pop125.json
 has pop1000 && run pop1000 1000 python bench.py --gpus 1 --pop-per-gpu 1000 --steps 2 --warmup 1 --dump-population gpurun_out/ev/pop1000.json
 has calib && run calib 900 python scripts/calibrate_cost.py --population-file populations/bench_pop1000_gen2.json --measure-ranks 8 --out gpurun_out/ev/cost_model.json
+has bench1 && run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
+has pop50 && run pop50 600 python bench.py --gpus 1 --pop-per-gpu 50 --parameters serann/parameters/experiment/example.json --steps ${BSTEPS:-3} --warmup 1
 has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
 exit 0
