@@ -57,6 +57,7 @@ def main():
     if dev == "cuda":
         torch.cuda.synchronize()
     todo = pool[a.per_engine:]
+    ev.timings = {k: 0.0 for k in ev.timings}
     t0 = time.perf_counter()
     res = []
     for i in range(0, len(todo), a.per_engine):
@@ -69,6 +70,7 @@ def main():
                       "genotypes": len(todo), "replicas_per_genotype": a.evaluations,
                       "offspring_per_replica": a.replications, "genotypes_per_engine": a.per_engine,
                       "reference_job_timeout_s": 800, "mean_val_acc": float(np.mean(acc)) if acc else None,
+                      "phase_seconds_per_genotype": {k: v / len(todo) for k, v in ev.timings.items()},
                       "device": dev, "data": "synthetic, table codec"}))
 
 

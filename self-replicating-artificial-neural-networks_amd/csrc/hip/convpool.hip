@@ -16,7 +16,8 @@
 // * WGRAD: dW[f][tap] = sum_{b,p} dz[b,p,f] [argmax == w] img[b][pos(p, w) + tap], one MFMA per
 //   (window offset, 32 pooled positions, 16 filters, 16 taps): A = dz masked by the argmax (held in
 //   registers across the window offsets), B = patches from LDS.  The bias gradient is the plain sum
-//   of dz.  Results are flushed with one Q32 fixed-point atomic per (wave, weight) (deterministic).
+//   of dz.  The waves' tiles are summed in LDS in wave order and flushed with one Q32 fixed-point
+//   atomic per (block, weight) (deterministic).
 // There is no DGRAD: the input is the raw image.
 //
 // One block = 4 waves = one organism x a chunk of images x a group of 64 filters.  Every wave owns
@@ -177,13 +178,15 @@ __global__ __launch_bounds__(256) void convpool_fwd_kernel(const ConvPoolDesc* _
     }
 
     bf16_t* slot = img[wave];
-    const int b0 = ic * CP_FWD_IMGS;
+    // images per block: d.flags when set (a multiple of 4, hip_ops.convpool_imgs), else CP_FWD_IMGS
+    const int ipb = d.flags > 0 ? (int)d.flags : CP_FWD_IMGS;
+    const int b0 = ic * ipb;
     CpStager st;
     st.start(d, b0 + wave, lane);
-    for (int it = 0; it < CP_FWD_IMGS / 4; ++it) {
+    for (int it = 0; it < ipb / 4; ++it) {
         const int b = b0 + it * 4 + wave;
         __syncthreads();
-        st.stage(d, slot, b, it + 1 < CP_FWD_IMGS / 4 ? b + 4 : Bn, lane);
+        st.stage(d, slot, b, it + 1 < ipb / 4 ? b + 4 : Bn, lane);
         __syncthreads();
         if (b >= Bn) continue;
         for (int pg = 0; pg < npos; pg += 16 * G) {
@@ -317,8 +320,8 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
     for (int nt = 0; nt < NT; ++nt) bsum[nt] = 0.f;
 
     bf16_t* slot = img[wave];
-    // images per block: d.flags when set (a multiple of 4: hip_ops.convpool_wgrad_imgs lowers it for
-    // launches of few blocks), else CP_WGRAD_IMGS
+    // images per block: d.flags when set (a multiple of 4: hip_ops.convpool_imgs lowers it until the
+    // problem has enough blocks to spread over the chip), else CP_WGRAD_IMGS
     const int ipb = d.flags > 0 ? (int)d.flags : CP_WGRAD_IMGS;
     const int b0 = ic * ipb;
     CpStager st;
@@ -406,21 +409,33 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
             }
         }
     }
-    // D[row = filter][col = tap]: lane holds filters 4*kg + r of tap column col
-    long long* __restrict__ dw = reinterpret_cast<long long*>(d.dw);     // Q32 gradient arena (common.h)
+    // D[row = filter][col = tap]: lane holds filters 4*kg + r of tap column col.  The 4 waves' tiles are
+    // summed in LDS in fixed wave order (deterministic), then flushed with one Q32 fixed-point atomic per
+    // (block, weight): with one image per wave (4-image blocks) per-wave flushes would cost 4x the atomics.
+    constexpr int RW = TT * 16;
+    __shared__ float red[NT * 16 * RW];
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
+            for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int tt = 0; tt < TT; ++tt) {
-            if (tt >= tts) break;
-            const int tap = tt * 16 + col;
-            if (tap >= taps) continue;
+                for (int tt = 0; tt < TT; ++tt) {
+                    if (tt >= tts) break;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int f = f0 + nt * 16 + kg * 4 + r;
-                if (f < F) fx_add(dw + (int64_t)f * taps + tap, acc[nt][tt][r]);
-            }
+                    for (int r = 0; r < 4; ++r) {
+                        const int e = (nt * 16 + kg * 4 + r) * RW + tt * 16 + col;
+                        red[e] = (w == 0 ? 0.f : red[e]) + acc[nt][tt][r];
+                    }
+                }
         }
+        __syncthreads();
+    }
+    long long* __restrict__ dw = reinterpret_cast<long long*>(d.dw);     // Q32 gradient arena (common.h)
+    const int tw = tts * 16;
+    for (int e = threadIdx.x; e < NT * 16 * tw; e += 256) {
+        const int row = e / tw, tap = e - row * tw;
+        const int f = f0 + row;
+        if (f < F && tap < taps) fx_add(dw + (int64_t)f * taps + tap, red[row * RW + tap]);
     }
     long long* __restrict__ dbias = reinterpret_cast<long long*>(d.dbias);
     if (dbias != nullptr) {

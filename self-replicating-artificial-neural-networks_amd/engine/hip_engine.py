@@ -28,6 +28,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..experiment.cost_model import organism_time
 from ..genome.ir import Node, OrganismIR
 from ..models.organism import glorot_limit, init_params
 from ..ops import hip_ops as H
@@ -586,12 +587,16 @@ class HipPopulationEngine(PopulationEngine):
         return fcat, fcons
 
     def _stream_groups(self, nstreams: int) -> List[List[int]]:
-        """Partition the organisms into <= nstreams groups of similar training FLOPs (LPT)."""
+        """Partition the organisms into <= nstreams groups of similar predicted step time (LPT on the
+        calibrated cost model; SERANN_STREAM_COST=flops: on training FLOPs, the round-2 rule)."""
         P = self.num_organisms
         k = max(1, min(int(nstreams), P))
         if k == 1:
             return [list(range(P))]
-        costs = [float(lay.ir.cost_per_sample()) + 1.0 for lay in self.layouts]
+        if os.environ.get("SERANN_STREAM_COST", "model") == "flops":
+            costs = [float(lay.ir.cost_per_sample()) + 1.0 for lay in self.layouts]
+        else:       # calibrated per-organism step time (experiment/cost_model.py), as for the rank partition
+            costs = [organism_time(lay.ir, self.cfg.batch_size) for lay in self.layouts]
         order = sorted(range(P), key=lambda o: -costs[o])
         loads = [0.0] * k
         groups: List[List[int]] = [[] for _ in range(k)]
@@ -760,7 +765,7 @@ class HipPopulationEngine(PopulationEngine):
             for kt in sorted(by_kt):
                 rws = by_kt[kt]
                 for r in rws:
-                    r["flags"] = H.convpool_wgrad_imgs(r["B"], r["F"]) if backward else 0
+                    r["flags"] = H.convpool_imgs(r["B"], r["F"], backward)
                 add_chunked("convpool", (1 if backward else 0, kt), rws, H.CONVPOOL_DTYPE,
                             [H.convpool_chunks(r["B"], r["F"], backward, r["flags"]) for r in rws], 1)
         def gchain_row(o, last):
@@ -1304,7 +1309,8 @@ class HipPopulationEngine(PopulationEngine):
         # descriptor / tile tables are uploaded from pageable host memory: fence them (and any
         # outstanding work on other streams) before a launch can read them.  Plans are built once per
         # generation, so this costs nothing on the training hot path.
-        torch.cuda.synchronize(self.device)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         return plan
 
     # ---------------------------------------------------------------------------------------------

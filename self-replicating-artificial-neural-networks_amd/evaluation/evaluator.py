@@ -19,6 +19,7 @@ invalid sources are not re-built (item 2).
 from __future__ import annotations
 
 import re
+import time
 from collections import Counter
 from typing import Dict, List, Optional, Sequence
 
@@ -73,6 +74,8 @@ class SerannEvaluator:
                                     int(experiment_params["genotype_size"]),
                                     int(experiment_params["num_classification_classes"]))
         self._validity: Dict[str, int] = {}
+        # wall seconds per phase, accumulated over evaluate_many calls (scripts/bench_evaluation.py)
+        self.timings: Dict[str, float] = {"engine_init": 0.0, "fit": 0.0, "replicate": 0.0, "host_post": 0.0}
 
     def is_valid_serann(self, source_code: str) -> int:
         v = self._validity.get(source_code)
@@ -115,14 +118,22 @@ class SerannEvaluator:
             # replica initialisations however run_many batches / de-duplicates / shards the sample
             keys = {i: genotype_key(genotypes[i]) for i, _ in owners}
             seeds = [organism_seed(self.seed, keys[i], f"eval{e}") for i, e in owners]
+            t0 = time.perf_counter()
             eng = make_engine(self.engine, irs, seeds, self.device, self.cfg)
+            t1 = time.perf_counter()
             try:
                 fit = eng.fit(self.data, self.cfg)
+                t2 = time.perf_counter()
                 imgs = [self.data.test_x[:self.R]] * len(irs)
                 gens = np.stack([genotypes[i] for i, _ in owners]).astype(np.float32)
                 outs = eng.replicate(gens, imgs, self.cfg)
+                t3 = time.perf_counter()
             finally:
                 eng.close()
+            self.timings["engine_init"] += t1 - t0
+            self.timings["fit"] += t2 - t1
+            self.timings["replicate"] += t3 - t2
+            t4 = time.perf_counter()
             by_sample: Dict[int, list] = {}
             for k, (i, e) in enumerate(owners):
                 by_sample.setdefault(i, []).append((fit.val_acc[k], outs[k]))
@@ -146,6 +157,7 @@ class SerannEvaluator:
                     mutation.append(dict(Counter(rates.tolist())))
                 results[i] = {"classification_accuracy": acc, "mutation_rate": mutation,
                               "offspring_survival": survival}
+            self.timings["host_post"] += time.perf_counter() - t4
         return results
 
 

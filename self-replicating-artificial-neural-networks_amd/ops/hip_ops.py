@@ -6,6 +6,7 @@ the engine *requires* the extension (it fails loudly instead of silently falling
 """
 from __future__ import annotations
 
+import os as _os
 import numpy as np
 
 from ..utils.native import load
@@ -201,7 +202,7 @@ def gchain_variant(f1: int, f2: int, taps: int):
 # launch: a problem's row blocking -- and so the grouping of its fp32 partial sums before they meet in the
 # fixed-point workspaces -- must not depend on which other organisms share the launch, or an organism would
 # train differently in a 2-rank shard than in the whole population (deterministic sharding)
-GCHAIN_BLOCKS = {0: 96, 1: 96, 2: 192, 3: 48}
+GCHAIN_BLOCKS = {0: 96, 1: 96, 2: 192, 3: int(_os.environ.get("SERANN_GCHAIN_BFULL_BLOCKS", "48"))}
 GCHAIN_GMAX = 8192                                        # gchain.hip GC_GMAX: staged genotype elements
 
 
@@ -239,22 +240,30 @@ def gchain_rpb(rows: int, mode: int, l1: int = 1, l0: int = 0) -> int:
 
 def convpool_chunks(batch: int, filters: int, backward: bool, imgs: int = 0) -> int:
     """Blocks of one fused conv+pool problem: image chunks x groups of 64 filters (``imgs``: images
-    per WGRAD block, default CONVPOOL_WGRAD_IMGS)."""
-    per = (imgs or CONVPOOL_WGRAD_IMGS) if backward else CONVPOOL_FWD_IMGS
+    per block, default CONVPOOL_WGRAD_IMGS / CONVPOOL_FWD_IMGS)."""
+    per = imgs or (CONVPOOL_WGRAD_IMGS if backward else CONVPOOL_FWD_IMGS)
     return -(-int(batch) // per) * -(-int(filters) // 64)
 
 
-CONVPOOL_MIN_CHUNKS = 16    # fused conv+pool WGRAD: blocks one problem should have at least
+# blocks one fused conv+pool problem should have at least.  At 16 (round 2) a B = 750 problem ran in 24
+# WGRAD / 47 FWD blocks -- one block per CU on under a fifth of the chip, 150-260 us each on the bench
+# population (profiles/r3b/launch_table_before.txt); 160 takes both down to 4 images per block (188 blocks)
+CONVPOOL_MIN_CHUNKS = int(_os.environ.get("SERANN_CONVPOOL_MIN_CHUNKS", "160"))
+
+
+def convpool_imgs(batch: int, filters: int, backward: bool) -> int:
+    """Images per block of one fused conv+pool problem: 32 (WGRAD) / 16 (FWD), halved (down to 4: one
+    image per wave) while the problem alone has fewer than CONVPOOL_MIN_CHUNKS blocks.  Per problem, so
+    the grouping of the WGRAD partial sums does not depend on the other problems of the launch
+    (deterministic sharding)."""
+    imgs = CONVPOOL_WGRAD_IMGS if backward else CONVPOOL_FWD_IMGS
+    while imgs > 4 and convpool_chunks(batch, filters, backward, imgs) < CONVPOOL_MIN_CHUNKS:
+        imgs //= 2
+    return imgs
 
 
 def convpool_wgrad_imgs(batch: int, filters: int) -> int:
-    """Images per block of one fused conv+pool WGRAD problem: 32, halved (down to 8) while the problem
-    alone has fewer than CONVPOOL_MIN_CHUNKS blocks.  Per problem, so the grouping of the per-wave fp32
-    partial sums does not depend on the other problems of the launch (deterministic sharding)."""
-    imgs = CONVPOOL_WGRAD_IMGS
-    while imgs > 8 and convpool_chunks(batch, filters, True, imgs) < CONVPOOL_MIN_CHUNKS:
-        imgs //= 2
-    return imgs
+    return convpool_imgs(batch, filters, True)
 
 
 def red_chunks(rows: int, channels: int) -> int:
@@ -419,7 +428,6 @@ def conv_wgrad_config(geo: dict, F: int):
 
 NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
 
-import os as _os
 # A/B switches for measurements and fault isolation (all paths are on by default)
 _OFF = set(filter(None, _os.environ.get("SERANN_GEMM3_OFF", "").split(",")))   # conv_fwd,conv_wgrad,narrow,sk
 

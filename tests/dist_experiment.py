@@ -1,6 +1,7 @@
 """Helper script for tests/test_gpu_distributed.py (run as a subprocess, one per rank): a short seeded
 experiment on the HIP engine; rank 0 writes the DB to argv[1].  The communicator comes from the
-environment (RANK / WORLD_SIZE / MASTER_*; SERANN_COMM_BACKEND=gloo lets two ranks share one GPU)."""
+environment (RANK / WORLD_SIZE / MASTER_*; SERANN_COMM_BACKEND=gloo lets two ranks share one GPU;
+SERANN_FORCE_DIST=1 with SERANN_COMM_BACKEND=nccl runs one rank through RCCL)."""
 import os
 import sys
 
@@ -18,7 +19,9 @@ def main(db_path: str, pop: int, gens: int):
     from serann.parallel.comm import make_comm
     from serann.utils.db import ExperimentDB
 
-    comm = make_comm()
+    # SERANN_FORCE_DIST=1: a torch.distributed communicator even for world_size 1 (RCCL on one GPU)
+    comm = make_comm(distributed=True if os.environ.get("SERANN_FORCE_DIST") == "1" else None)
+    print(f"comm backend={getattr(comm, 'backend', 'local')} world={comm.world_size}", flush=True)
     device = default_device(comm)
     enc = synthetic_encodings()
     data = get_serann_data(enc, synthetic_mnist(n_train=2400, n_test=400, seed=3), n_train=2400, n_test=400)

@@ -26,13 +26,15 @@ def _free_port():
     return port
 
 
-def _launch(db, world, pop, gens):
+def _launch(db, world, pop, gens, backend="gloo"):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), SERANN_COMM_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-        if world == 1:
+                   MASTER_PORT=str(port), SERANN_COMM_BACKEND=backend, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if backend == "nccl":
+            env["SERANN_FORCE_DIST"] = "1"
+        elif world == 1:
             for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
                 env.pop(k)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_experiment.py"), str(db), str(pop),
@@ -63,3 +65,17 @@ def test_two_ranks_write_the_single_rank_db(tmp_path):
             "genotype_nucleotide_diversity, source_code_species_richness")
     pd.testing.assert_frame_equal(pd.read_sql(f"select {cols} from generations", sqlite3.connect(one)),
                                   pd.read_sql(f"select {cols} from generations", sqlite3.connect(two)))
+
+
+def test_rccl_communicator_with_hip_engine(tmp_path):
+    """The RCCL (``nccl``) communicator in the same process as the HIP engine's captured graphs and
+    side streams: one rank through torch.distributed over RCCL -- length all-gather, packed
+    ``all_gather_into_tensor`` of the device payload, broadcasts, barrier -- writes the same DB as the
+    plain local communicator.  (Two RCCL ranks cannot share one GPU; the 2-rank schedule is covered by
+    the gloo test above and the multi-GPU bench.)"""
+    local, rccl = tmp_path / "local.sqlite", tmp_path / "rccl.sqlite"
+    _launch(local, 1, 8, 2)
+    out = _launch(rccl, 1, 8, 2, backend="nccl")
+    assert "comm backend=nccl world=1" in out[0], out[0][-2000:]
+    q = "select * from serann order by generation, id"
+    pd.testing.assert_frame_equal(pd.read_sql(q, sqlite3.connect(local)), pd.read_sql(q, sqlite3.connect(rccl)))

@@ -72,7 +72,8 @@ def test_decomposition_is_per_problem():
         assert _split_signature(H.MODE_FWD, [r], [d])[r["out"]] == full[r["out"]]
     # fused chain and conv+pool: functions of the problem alone
     assert H.gchain_rpb(72000, H.GC_BFULL, 96, 100) == H.gchain_rpb(72000, H.GC_BFULL, 96, 100)
-    assert H.convpool_wgrad_imgs(750, 32) == 32 and H.convpool_wgrad_imgs(80, 16) == 8
+    assert H.convpool_wgrad_imgs(750, 32) == 4 and H.convpool_wgrad_imgs(80, 16) == 4
+    assert H.convpool_imgs(750, 80, False) == 8 and H.convpool_imgs(4000, 32, True) == 16
 
 
 def test_gchain_large_genotype_is_not_fused():
