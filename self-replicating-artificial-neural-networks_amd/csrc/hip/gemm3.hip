@@ -786,17 +786,21 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
 // A fragment (output pixel x 8 channels of one tap) is then one aligned ds_read_b128 -- the kh*kw-fold
 // re-reads of im2col are served by LDS instead of the vector-memory pipeline, and odd channel counts
 // no longer produce misaligned global loads.  The reduction runs over (tap, padded channel) in
-// 32-element MFMA k-steps; the matching weight tile [BN][32] is staged in LDS once per block and
-// step (double-buffered, one barrier per step) and shared by the 4 waves.
+// 32-element MFMA k-steps; the weights are staged in LDS in chunks of KC k-steps ([BN][KC * 32],
+// double-buffered, one barrier and one round of global loads per chunk) shared by the 4 waves.
 // PATCH = LDS patch capacity in bf16 elements: 8192 / 16384 / 32768 (16 / 32 / 64 KB; with the weight
 // tiles that allows about 8 / 4 / 2 resident blocks per CU).
 template <int NT, int RT, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __restrict__ descs,
                                                           const int4* __restrict__ tiles) {
-    constexpr int TM = 64 * RT, BN = NT * 16, LDBS = 40;
+    constexpr int TM = 64 * RT, BN = NT * 16;
+    // k-steps per weight chunk: the weight buffers stay near 10 KB with the 64 KB patch tier (two blocks
+    // per CU) and near 17 KB with the smaller tiers
+    constexpr int KC = (PATCH >= 32768 ? 4 : 8) / NT;
+    constexpr int LDBC = KC * 32 + 8;                   // weight row stride: an odd number of 16-B slots
     // the patch region doubles as the output staging tile after the k loop
     __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH > TM * BN ? PATCH : TM * BN];
-    __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN * LDBS];
+    __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN * LDBC];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);
@@ -838,20 +842,44 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
         rowoff[i] = ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
     }
 
-    // ---- weight tile loader: thread -> (column bn, 8-element chunk bkg) --------------------------
+    // ---- weight chunks: KC k-steps of the [BN][32] weight tile per LDS buffer (double-buffered) ----
+    // One barrier and one round of global loads per chunk instead of per k-step: with 1-4 MFMAs per
+    // wave and k-step (BN = 16..64), a per-step barrier with the next step's weights loaded only one step
+    // ahead left the loop waiting on load latency (round-3 roofline: 5-8 % MFMA busy, ~1 TB/s).
     const int taps = g.KH * g.KW;
     const int nsteps = (taps * Cp + 31) / 32;
+    const int nchunks = (nsteps + KC - 1) / KC;
     const rsrc_t rB = mkrsrc(d.b, (int64_t)g.N * g.K * 2);
-    const int bn = t >> 2, bkg = (t & 3) * 8;
-    const int brow = min(n0 + bn, g.N - 1) * g.K;
-    auto gload_b = [&](int s) -> uint4 {
-        const int e = s * 32 + bkg;
-        const int tap = fdiv(e, dCp);
-        const int c = e - tap * Cp;
-        if (bn >= BN || tap >= taps || c >= g.C) return zero;
-        uint4 v = bl16(rB, brow + tap * g.C + c);
-        if (c + 8 > g.C) v = splice(v, zero, g.C - c);
-        return v;
+    constexpr int PPR = KC * 4;                         // 8-element pieces per weight row and chunk
+    constexpr int NPC = BN * PPR / 256;                 // pieces per thread and chunk
+    static_assert(NPC * 256 == BN * PPR, "weight chunk must split evenly over the block");
+    int brow[NPC], bcol[NPC];
+#pragma unroll
+    for (int q = 0; q < NPC; ++q) {
+        const int pc = t + q * 256;
+        const int bn = pc / PPR;
+        bcol[q] = (pc - bn * PPR) * 8;
+        brow[q] = bn;
+    }
+    auto gload_chunk = [&](int ch, uint4 (&r)[NPC]) {
+#pragma unroll
+        for (int q = 0; q < NPC; ++q) {
+            const int e = ch * KC * 32 + bcol[q];
+            const int tap = fdiv(e, dCp);
+            const int c = e - tap * Cp;
+            const int n = n0 + brow[q];
+            if (n >= g.N || tap >= taps || c >= g.C) {
+                r[q] = zero;
+            } else {
+                uint4 v = bl16(rB, n * g.K + tap * g.C + c);
+                if (c + 8 > g.C) v = splice(v, zero, g.C - c);
+                r[q] = v;
+            }
+        }
+    };
+    auto stash_chunk = [&](int buf, const uint4 (&r)[NPC]) {
+#pragma unroll
+        for (int q = 0; q < NPC; ++q) *reinterpret_cast<uint4*>(&Bs[buf][brow[q] * LDBC + bcol[q]]) = r[q];
     };
 
     f32x4_t acc[RT][NT];
@@ -860,31 +888,35 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    uint4 breg = gload_b(0);
-    if (bn < BN) *reinterpret_cast<uint4*>(&Bs[0][bn * LDBS + bkg]) = breg;
+    uint4 breg[NPC];
+    gload_chunk(0, breg);
+    stash_chunk(0, breg);
     __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-        const int cur = s & 1;
-        if (s + 1 < nsteps) breg = gload_b(s + 1);
-        const int e = s * 32 + kg;
-        int tap = fdiv(e, dCp);
-        const int c = e - tap * Cp;
-        tap = min(tap, taps - 1);                       // past the end: finite A, zero B
-        const int kh = fdiv(tap, g.dKW);
-        const int kw = tap - kh * g.KW;
-        const int tapoff = (kh * g.W + kw) * Cs + c;
-        Frag fa[RT], fb[NT];
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < nchunks) gload_chunk(ch + 1, breg);
+        const int s_end = min(KC, nsteps - ch * KC);
+        for (int sl = 0; sl < s_end; ++sl) {
+            const int e = (ch * KC + sl) * 32 + kg;
+            int tap = fdiv(e, dCp);
+            const int c = e - tap * Cp;
+            tap = min(tap, taps - 1);                   // past the end: finite A, zero B
+            const int kh = fdiv(tap, g.dKW);
+            const int kw = tap - kh * g.KW;
+            const int tapoff = (kh * g.W + kw) * Cs + c;
+            Frag fa[RT], fb[NT];
 #pragma unroll
-        for (int i = 0; i < RT; ++i) fa[i].u = *reinterpret_cast<const uint4*>(&patch[rowoff[i] + tapoff]);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-            fb[j].u = *reinterpret_cast<const uint4*>(&Bs[cur][(j * 16 + r16) * LDBS + kg]);
-#pragma unroll
-        for (int i = 0; i < RT; ++i)
+            for (int i = 0; i < RT; ++i) fa[i].u = *reinterpret_cast<const uint4*>(&patch[rowoff[i] + tapoff]);
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
-        if (s + 1 < nsteps && bn < BN) *reinterpret_cast<uint4*>(&Bs[cur ^ 1][bn * LDBS + bkg]) = breg;
+                fb[j].u = *reinterpret_cast<const uint4*>(&Bs[cur][(j * 16 + r16) * LDBC + sl * 32 + kg]);
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
+        }
+        if (ch + 1 < nchunks) stash_chunk(cur ^ 1, breg);
         __syncthreads();
     }
 
