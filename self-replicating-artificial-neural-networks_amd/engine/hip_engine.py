@@ -642,11 +642,7 @@ class HipPopulationEngine(PopulationEngine):
             return t
 
         def desc_tensor(rows, dtype):
-            a = np.zeros(len(rows), dtype=dtype)
-            for i, r in enumerate(rows):
-                for k, v in r.items():
-                    if not k.startswith("_"):
-                        a[i][k] = v
+            a = H.record_array(rows, dtype)
             if dtype == H.GEMM_DTYPE:
                 H.fill_gemm_divisors(a)
             return T(np.frombuffer(a.tobytes(), dtype=np.uint8).copy())

@@ -6,6 +6,7 @@ the engine *requires* the extension (it fails loudly instead of silently falling
 """
 from __future__ import annotations
 
+import functools
 import os as _os
 import numpy as np
 
@@ -57,6 +58,7 @@ POOL_ELEMS = 1024
 COPY_ROWS = 16
 
 
+@functools.lru_cache(maxsize=4096)
 def fast_div_magic(d: int) -> int:
     """Packed (multiplier | shift << 32) for q = (umulhi(n, mul) + n) >> shift == n // d, exact for
     0 <= n < 2**31 (gemm3.hip fdiv)."""
@@ -66,30 +68,39 @@ def fast_div_magic(d: int) -> int:
     return int(mul | (sh << 32))
 
 
+_DIVISOR_FIELDS = (("dvC", lambda a: a["C"]), ("dvKW", lambda a: a["KW"]), ("dvOW", lambda a: a["OW"]),
+                   ("dvOHW", lambda a: a["OH"] * a["OW"]), ("dvF", lambda a: a["F"]), ("dvW", lambda a: a["W"]),
+                   ("dvHW", lambda a: a["H"] * a["W"]), ("dvSH", lambda a: a["SH"]), ("dvSW", lambda a: a["SW"]),
+                   ("dvCp", lambda a: -(-a["C"] // 8) * 8))
+
+
 def fill_gemm_divisors(a: np.ndarray) -> np.ndarray:
     """Fill the dv* fields of a GEMM_DTYPE record array from its geometry fields (in place)."""
-    for r in a:
-        r["dvC"] = fast_div_magic(r["C"])
-        r["dvKW"] = fast_div_magic(r["KW"])
-        r["dvOW"] = fast_div_magic(r["OW"])
-        r["dvOHW"] = fast_div_magic(r["OH"] * r["OW"])
-        r["dvF"] = fast_div_magic(r["F"])
-        r["dvW"] = fast_div_magic(r["W"])
-        r["dvHW"] = fast_div_magic(r["H"] * r["W"])
-        r["dvSH"] = fast_div_magic(r["SH"])
-        r["dvSW"] = fast_div_magic(r["SW"])
-        r["dvCp"] = fast_div_magic(-(-int(r["C"]) // 8) * 8)
+    for name, src in _DIVISOR_FIELDS:
+        a[name] = [fast_div_magic(int(v)) for v in src(a)]
+    return a
+
+
+def record_array(rows, dtype) -> np.ndarray:
+    """dict rows -> structured records of ``dtype`` (keys starting with '_' are planner annotations and
+    skipped; missing fields are 0; an unknown field raises), filled column by column."""
+    a = np.zeros(len(rows), dtype=dtype)
+    keys = set()
+    for r in rows:
+        keys.update(r)
+    names = set(dtype.names)
+    for k in keys:
+        if k.startswith("_"):
+            continue
+        if k not in names:
+            raise ValueError(f"no field of name {k}")
+        a[k] = [r.get(k, 0) for r in rows]
     return a
 
 
 def gemm_desc_array(rows) -> np.ndarray:
     """dict rows -> GEMM_DTYPE records with the fast-division fields filled."""
-    a = np.zeros(len(rows), dtype=GEMM_DTYPE)
-    for i, r in enumerate(rows):
-        for k, v in r.items():
-            if not k.startswith("_"):
-                a[i][k] = v
-    return fill_gemm_divisors(a)
+    return fill_gemm_divisors(record_array(rows, GEMM_DTYPE))
 
 
 BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256) BatchNorm kernel
@@ -572,12 +583,15 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             # every block restages its patches and the cross-chunk prefetch needs a long chunk range)
             for p, (r, (M, N, K)) in enumerate(items):
                 nchunks, nkt, nft, per = geo[p]
-                for c0 in range(0, nchunks, per):
-                    c1 = min(nchunks, c0 + per)
-                    ff, kk = np.meshgrid(np.arange(nft), np.arange(nkt), indexing="ij")
-                    n = ff.size
-                    tl.append(np.stack([np.full(n, p), (ff.ravel() << 16) | kk.ravel(), np.full(n, c0),
-                                        np.full(n, c1)], 1))
+                # tiles ordered (chunk range, f tile, k' tile), vectorised over all three
+                c0 = np.arange(0, nchunks, per)
+                fk = ((np.arange(nft)[:, None] << 16) | np.arange(nkt)[None, :]).ravel()
+                t_ = np.empty((len(c0), len(fk), 4), np.int64)
+                t_[..., 0] = p
+                t_[..., 1] = fk[None, :]
+                t_[..., 2] = c0[:, None]
+                t_[..., 3] = np.minimum(nchunks, c0 + per)[:, None]
+                tl.append(t_.reshape(-1, 4))
             tiles = np.concatenate(tl).astype(np.int32)
         else:
             bm, bn = gemm3_block(mode, v)
