@@ -674,11 +674,6 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
     sums that meet in the fixed-point arena, so they must not depend on the launch (deterministic
     sharding)."""
     tg = _WGRAD_TARGET
-    if K and int(K) >= WGRAD_STREAM_ROWS:
-        # streaming problems (a small weight matrix over 10^5 rows): short blocks.  At 128 k-steps the
-        # largest problem of a launch ran 64 serial 64-row steps per block while the rest of the chip had
-        # drained (bench population: a 300000-row [60 x 16] WGRAD set the 238 us of its launch)
-        tg = min(tg, WGRAD_STREAM_TARGET)
     tiles = -(-int(M) // bm) * -(-int(N) // bn)
     while tg > 16 and K and tiles * wgrad_splits(K, tg, min(32, tg)) < WGRAD_MIN_BLOCKS:
         tg //= 2
@@ -686,8 +681,6 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
-WGRAD_STREAM_ROWS = int(_os.environ.get("SERANN_WGRAD_STREAM_ROWS", "32768"))   # reduction rows
-WGRAD_STREAM_TARGET = int(_os.environ.get("SERANN_WGRAD_STREAM_TARGET", "32"))  # k-steps per block
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
