@@ -434,7 +434,7 @@ def conv_wgrad_config(geo: dict, F: int):
         bnk = 256 if kp > 128 else 128
     else:
         bnk = 512 if kp >= 384 else (256 if kp > 128 else 128)
-    return bmf, bnk, tier
+    return bmf, min(bnk, CONV_WGRAD_BNK_MAX), tier
 
 
 NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
@@ -578,7 +578,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 cp = -(-int(r["C"]) // 8) * 8
                 nkt = -(-(int(r["KH"]) * int(r["KW"]) * cp) // bnk)
                 nft = -(-M // bmf)
-                geo.append((nchunks, nkt, nft, min(64, max(8, -(-nchunks // 64)))))
+                geo.append((nchunks, nkt, nft, min(CONV_WGRAD_MAXPER, max(8, -(-nchunks // CONV_WGRAD_SPLITS)))))
             # (chunks per block 8..64: unlike the GEMM WGRAD, more and shorter blocks measured slower --
             # every block restages its patches and the cross-chunk prefetch needs a long chunk range)
             for p, (r, (M, N, K)) in enumerate(items):
@@ -681,6 +681,11 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+# conv-halo WGRAD: chunk-range splits per problem (8..CONV_WGRAD_MAXPER 128-row chunks per block)
+CONV_WGRAD_SPLITS = int(_os.environ.get("SERANN_CONV_WGRAD_SPLITS", "64"))
+CONV_WGRAD_MAXPER = int(_os.environ.get("SERANN_CONV_WGRAD_MAXPER", "64"))
+# k' tile width cap: 256 measured 14.56 vs 14.61 ms (4 streams), 18.3 vs 18.6 (1 stream), 12 fewer launches
+CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "256"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
