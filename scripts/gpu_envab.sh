@@ -15,6 +15,6 @@ for round in 1 2; do
   for c in "${CFG[@]}"; do
     i=$((i+1))
     env $c timeout -k 10 200 python scripts/bench_step.py --population-file $POP --streams ${STREAMS:-4,1} --epochs ${EPOCHS:-2} > gpurun_out/envab/r${round}_c$i.log 2>&1 || { echo "config '$c' failed"; tail -8 gpurun_out/envab/r${round}_c$i.log; exit 1; }
-    grep streams= gpurun_out/envab/r${round}_c$i.log | sed "s/^/[$c] /"
+    grep streams= gpurun_out/envab/r${round}_c$i.log | while read -r l; do echo "[$c] $l"; done
   done
 done

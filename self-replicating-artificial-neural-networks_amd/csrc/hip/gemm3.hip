@@ -29,6 +29,9 @@
 #ifndef WG_NSETS
 #define WG_NSETS 2          // WGRAD register sets in flight (build-time A/B knob)
 #endif
+#ifndef WG_RG
+#define WG_RG 2             // WGRAD row groups per block (hip_ops.WGRAD_ROW_GROUPS must match)
+#endif
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
@@ -500,21 +503,32 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
 // step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
 // in LDS in that layout with 16-B writes; MFMA fragments come from ds_read_b64_tr_b16.
 template <int BMF, int BNK, bool GEN, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
-                                                       const int4* __restrict__ tiles) {
+__global__ __launch_bounds__(64 * NWV * WG_RG) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                               const int4* __restrict__ tiles) {
     constexpr int BKM = 64;
-    constexpr int NTH = 64 * NWV;                    // threads per block (NWV = 8: wide f tiles, 2 x 4 waves)
+    constexpr int NTH = 64 * NWV;                    // threads per row group
+    constexpr int RG = WG_RG;                        // row groups per block
     constexpr int LDA = BMF + 8, LDB = BNK + 8;
-    __shared__ __attribute__((aligned(16))) bf16_t As[BKM * LDA];
-    __shared__ __attribute__((aligned(16))) bf16_t Bs[BKM * LDB];
+    constexpr int SMEM = RG * BKM * (LDA + LDB);     // bf16 elements: one As / Bs pair per row group
+    __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
+    const int rg = threadIdx.x / NTH;
+    bf16_t* __restrict__ As = smem + rg * BKM * (LDA + LDB);
+    bf16_t* __restrict__ Bs = As + BKM * LDA;
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
     const int f0 = td.y * BMF, k0c = td.z * BNK;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // in units of 32 rows of m
-    const int mlim = min(g.K, kt1 * 32);
+    // Row groups (RG = 2): the block's k range is split into contiguous halves of whole 64-row steps, one
+    // per group of NWV waves with its own LDS tiles; the groups' tiles are summed in LDS (group order)
+    // before the one flush per block -- half the fixed-point atomics of two separate blocks at the same
+    // parallelism.  Every group runs group 0's step count (same barrier sequence); loads past its own
+    // range are masked to zeros.
+    const int kh = RG > 1 ? ((kt1 - kt0 + 2 * RG - 1) / (2 * RG)) * 2 : kt1 - kt0;
+    const int gk0 = min(kt1, kt0 + rg * kh), gk1 = min(kt1, gk0 + kh);
+    const int mlim = min(g.K, gk1 * 32);
     long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x - rg * NTH, lane = t & 63, wave = t >> 6;
     const int ohw = g.OH * g.OW;
     const int64_t nb = g.K / ohw;                              // batch
     const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
@@ -671,43 +685,72 @@ __global__ __launch_bounds__(64 * NWV) void g3_wgrad_kernel(const GemmDesc* __re
 
     // kt counts 32-row units; one step consumes two of them (64 rows); steps rotate over WG_NSETS
     // register sets, so the loads of a step are issued WG_NSETS steps before it is staged
+    const int ks = kt0 + rg * kh, ke = ks + kh;      // this group's steps (past gk1: masked loads)
 #if WG_NSETS == 2
-    if (kt0 < kt1) load(kt0, ra0, ry0, rb0);
-    if (kt0 + 2 < kt1) load(kt0 + 2, ra1, ry1, rb1);
-    for (int kt = kt0; kt < kt1; kt += 4) {
+    if (ks < ke) load(ks, ra0, ry0, rb0);
+    if (ks + 2 < ke) load(ks + 2, ra1, ry1, rb1);
+    for (int kt = ks; kt < ke; kt += 4) {
         __syncthreads();
         stash(ra0, ry0, rb0);
         bias_acc(ra0);
         __syncthreads();
-        if (kt + 4 < kt1) load(kt + 4, ra0, ry0, rb0);
+        if (kt + 4 < ke) load(kt + 4, ra0, ry0, rb0);
         compute();
-        if (kt + 2 >= kt1) break;
+        if (kt + 2 >= ke) break;
         __syncthreads();
         stash(ra1, ry1, rb1);
         bias_acc(ra1);
         __syncthreads();
-        if (kt + 6 < kt1) load(kt + 6, ra1, ry1, rb1);
+        if (kt + 6 < ke) load(kt + 6, ra1, ry1, rb1);
         compute();
     }
 #else
     Frag rax[WG_NSETS][APASS], ryx[WG_NSETS][APASS], rbx[WG_NSETS][BPASS];
 #pragma unroll
     for (int q_ = 0; q_ < WG_NSETS; ++q_)
-        if (kt0 + 2 * q_ < kt1) load(kt0 + 2 * q_, rax[q_], ryx[q_], rbx[q_]);
-    for (int kt = kt0; kt < kt1; kt += 2 * WG_NSETS) {
+        if (ks + 2 * q_ < ke) load(ks + 2 * q_, rax[q_], ryx[q_], rbx[q_]);
+    for (int kt = ks; kt < ke; kt += 2 * WG_NSETS) {
 #pragma unroll
         for (int q_ = 0; q_ < WG_NSETS; ++q_) {
             const int kc = kt + 2 * q_;
-            if (kc >= kt1) break;
+            if (kc >= ke) break;
             __syncthreads();
             stash(rax[q_], ryx[q_], rbx[q_]);
             bias_acc(rax[q_]);
             __syncthreads();
-            if (kc + 2 * WG_NSETS < kt1) load(kc + 2 * WG_NSETS, rax[q_], ryx[q_], rbx[q_]);
+            if (kc + 2 * WG_NSETS < ke) load(kc + 2 * WG_NSETS, rax[q_], ryx[q_], rbx[q_]);
             compute();
         }
     }
 #endif
+    if constexpr (RG > 1) {
+        // group 1 hands its accumulators and bias sums to group 0 through LDS (the tiles are free now)
+        constexpr int PER = TF * TK * 4 + 8;
+        static_assert(NTH * PER * 4 <= SMEM * 2, "row-group reduction must fit in the LDS tiles");
+        static_assert(RG == 2, "two row groups");
+        float* red = reinterpret_cast<float*>(smem);
+        __syncthreads();
+        if (rg == 1) {
+#pragma unroll
+            for (int i = 0; i < TF; ++i)
+#pragma unroll
+                for (int j = 0; j < TK; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) red[((i * TK + j) * 4 + r) * NTH + t] = acc[i][j][r];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) red[(TF * TK * 4 + j) * NTH + t] = bsum[j];
+        }
+        __syncthreads();
+        if (rg == 1) return;
+#pragma unroll
+        for (int i = 0; i < TF; ++i)
+#pragma unroll
+            for (int j = 0; j < TK; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((i * TK + j) * 4 + r) * NTH + t];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += red[(TF * TK * 4 + j) * NTH + t];
+    }
 
     if (do_bias) {
         if ((ACH & (ACH - 1)) == 0) {
@@ -2025,6 +2068,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     if (mode == MODE_WGRAD) {
         const bool gen = variant >= 1000000;
         const int v = variant % 1000000;
+        block = dim3(256 * WG_RG);
 #define W3(BMF_, BNK_) \
     if (v == BMF_ * 1000 + BNK_) { \
         if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \

@@ -680,13 +680,16 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
     return tg
 
 
-_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+# gemm3.hip WG_RG: row groups of 4 waves per WGRAD block; a block walks WGRAD_ROW_GROUPS x 128 k-steps
+# (128 per group), so an m-split costs one fixed-point flush per 2 x 128 k-steps
+WGRAD_ROW_GROUPS = int(_os.environ.get("SERANN_WGRAD_ROW_GROUPS", "2"))
+_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", str(128 * WGRAD_ROW_GROUPS)))
 # conv-halo WGRAD: chunk-range splits per problem (8..CONV_WGRAD_MAXPER 128-row chunks per block)
 CONV_WGRAD_SPLITS = int(_os.environ.get("SERANN_CONV_WGRAD_SPLITS", "64"))
 CONV_WGRAD_MAXPER = int(_os.environ.get("SERANN_CONV_WGRAD_MAXPER", "64"))
 # k' tile width cap: 256 measured 14.56 vs 14.61 ms (4 streams), 18.3 vs 18.6 (1 stream), 12 fewer launches
 CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "256"))
-WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem
+WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", str(64 // WGRAD_ROW_GROUPS)))  # per problem
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
