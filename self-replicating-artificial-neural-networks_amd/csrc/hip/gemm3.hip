@@ -29,9 +29,6 @@
 #ifndef WG_NSETS
 #define WG_NSETS 2          // WGRAD register sets in flight (build-time A/B knob)
 #endif
-#ifndef WG_RG
-#define WG_RG 2             // WGRAD row groups per block (hip_ops.WGRAD_ROW_GROUPS must match)
-#endif
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
@@ -502,12 +499,11 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
 // WGRAD: dWm[f][k] += sum_m dZ[m][f] * im2col(X)[m][k].  Tile BMF (f) x BNK (k), 64 rows of m per
 // step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
 // in LDS in that layout with 16-B writes; MFMA fragments come from ds_read_b64_tr_b16.
-template <int BMF, int BNK, bool GEN, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV * WG_RG) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
-                                                               const int4* __restrict__ tiles) {
+template <int BMF, int BNK, bool GEN, int NWV = 4, int RG = 1>
+__global__ __launch_bounds__(64 * NWV * RG) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                            const int4* __restrict__ tiles) {
     constexpr int BKM = 64;
-    constexpr int NTH = 64 * NWV;                    // threads per row group
-    constexpr int RG = WG_RG;                        // row groups per block
+    constexpr int NTH = 64 * NWV;                    // threads per row group (RG row groups per block)
     constexpr int LDA = BMF + 8, LDB = BNK + 8;
     constexpr int SMEM = RG * BKM * (LDA + LDB);     // bf16 elements: one As / Bs pair per row group
     __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
@@ -519,11 +515,12 @@ __global__ __launch_bounds__(64 * NWV * WG_RG) void g3_wgrad_kernel(const GemmDe
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
     const int f0 = td.y * BMF, k0c = td.z * BNK;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // in units of 32 rows of m
-    // Row groups (RG = 2): the block's k range is split into contiguous halves of whole 64-row steps, one
-    // per group of NWV waves with its own LDS tiles; the groups' tiles are summed in LDS (group order)
-    // before the one flush per block -- half the fixed-point atomics of two separate blocks at the same
-    // parallelism.  Every group runs group 0's step count (same barrier sequence); loads past its own
-    // range are masked to zeros.
+    // Row groups (RG = 2, m-split problems): the block's k range is split into contiguous halves of whole
+    // 64-row steps, one per group of NWV waves with its own LDS tiles; the groups' tiles are summed in LDS
+    // (group order) before the one flush per block -- half the fixed-point atomics of two separate blocks
+    // at the same parallelism.  Every group runs group 0's step count (same barrier sequence); loads past
+    // its own range are masked to zeros.  Single-split problems (plain store / fused Adam) keep RG = 1:
+    // their 750-row reductions ran 11 % slower per step as two half-length groups (ancestor population).
     const int kh = RG > 1 ? ((kt1 - kt0 + 2 * RG - 1) / (2 * RG)) * 2 : kt1 - kt0;
     const int gk0 = min(kt1, kt0 + rg * kh), gk1 = min(kt1, gk0 + kh);
     const int mlim = min(g.K, gk1 * 32);
@@ -2068,11 +2065,16 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     if (mode == MODE_WGRAD) {
         const bool gen = variant >= 1000000;
         const int v = variant % 1000000;
-        block = dim3(256 * WG_RG);
+        // v = BMF * 1000 + BNK (+ 500: two row groups per block, 512 threads)
 #define W3(BMF_, BNK_) \
     if (v == BMF_ * 1000 + BNK_) { \
         if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return; } \
+    if (v == BMF_ * 1000 + BNK_ + 500) { \
+        const dim3 b2(512); \
+        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true, 4, 2>), grid, b2, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 4, 2>), grid, b2, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
 #undef W3

@@ -541,6 +541,10 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
+            if mode == MODE_WGRAD:
+                bm_, bn_ = gemm3_block(mode, v)
+                if wgrad_row_groups(M, N, K, bm_, bn_) == 2:
+                    v += 500
         groups.setdefault(v, []).append((r, dm))
     _merge_tiled_widths(groups)
     out = []
@@ -597,7 +601,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             bm, bn = gemm3_block(mode, v)
             dms = [dm for _, dm in items]
             if mode == MODE_WGRAD:
-                tg = [wgrad_target(M, N, K, bm, bn) for (M, N, K) in dms]
+                rg = 2 if (v % 1000000) % 1000 >= 500 else 1
+                tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     if wgrad_splits(K, t_, min(32, t_)) == 1:
@@ -666,30 +671,40 @@ def wgrad_splits(K: int, target_ksteps: int = 128, min_ksteps: int = 32) -> int:
     return max(1, min(-(-kt // min_ksteps), -(-kt // target_ksteps), _WGRAD_MAXSPLIT))
 
 
-def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64) -> int:
+def wgrad_row_groups(M: int, N: int, K: int, bm: int, bn: int) -> int:
+    """Row groups per block of a Dense / 1x1 WGRAD problem: 2 when it is m-split at one group per block
+    (the groups halve its fixed-point flushes), 1 for single-split problems (plain store / fused Adam).
+    A function of the problem alone (deterministic sharding)."""
+    if WGRAD_ROW_GROUPS < 2:
+        return 1
+    tg = wgrad_target(M, N, K, bm, bn)
+    return 2 if wgrad_splits(K, tg, min(32, tg)) > 1 else 1
+
+
+def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64, rg: int = 1) -> int:
     """k-steps (32 rows) per WGRAD block: SERANN_WGRAD_TARGET (128), halved (down to 16) while the
     problem alone has fewer than WGRAD_MIN_BLOCKS blocks -- a small weight matrix over many rows
     (measured: two [70 x 98] Dense WGRADs over 75000 rows in 57 blocks ran at 0.2 TB/s) splits its
     reduction finer.  A function of the problem alone: the m-split boundaries decide the fp32 partial
     sums that meet in the fixed-point arena, so they must not depend on the launch (deterministic
     sharding)."""
-    tg = _WGRAD_TARGET
+    tg = _WGRAD_TARGET * rg
     tiles = -(-int(M) // bm) * -(-int(N) // bn)
-    while tg > 16 and K and tiles * wgrad_splits(K, tg, min(32, tg)) < WGRAD_MIN_BLOCKS:
+    while tg > 16 and K and tiles * wgrad_splits(K, tg, min(32, tg)) < WGRAD_MIN_BLOCKS // rg:
         tg //= 2
     return tg
 
 
-# gemm3.hip WG_RG: row groups of 4 waves per WGRAD block; a block walks WGRAD_ROW_GROUPS x 128 k-steps
-# (128 per group), so an m-split costs one fixed-point flush per 2 x 128 k-steps
+_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+# m-split WGRAD problems run two row groups of 4 waves per block (gemm3.hip, variant + 500): a block walks
+# 2 x 128 k-steps, so an m-split costs one fixed-point flush per 256 k-steps at the same parallelism
 WGRAD_ROW_GROUPS = int(_os.environ.get("SERANN_WGRAD_ROW_GROUPS", "2"))
-_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", str(128 * WGRAD_ROW_GROUPS)))
 # conv-halo WGRAD: chunk-range splits per problem (8..CONV_WGRAD_MAXPER 128-row chunks per block)
 CONV_WGRAD_SPLITS = int(_os.environ.get("SERANN_CONV_WGRAD_SPLITS", "64"))
 CONV_WGRAD_MAXPER = int(_os.environ.get("SERANN_CONV_WGRAD_MAXPER", "64"))
 # k' tile width cap: 256 measured 14.56 vs 14.61 ms (4 streams), 18.3 vs 18.6 (1 stream), 12 fewer launches
 CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "256"))
-WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", str(64 // WGRAD_ROW_GROUPS)))  # per problem
+WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem (4-wave blocks)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
