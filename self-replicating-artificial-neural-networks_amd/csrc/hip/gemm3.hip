@@ -776,28 +776,47 @@ __global__ __launch_bounds__(64 * NWV * RG) void g3_wgrad_kernel(const GemmDesc*
         // Q32 arena would hold it) -- the arena-wide Adam pass skips these parameters
         const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
         const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
-        float* P = reinterpret_cast<float*>(ac.p);
-        float* Mo = reinterpret_cast<float*>(ac.m);
-        float* Vo = reinterpret_cast<float*>(ac.v);
-        bf16_t* Pb = reinterpret_cast<bf16_t*>(ac.pbf);
+        float* __restrict__ P = reinterpret_cast<float*>(ac.p);
+        float* __restrict__ Mo = reinterpret_cast<float*>(ac.m);
+        float* __restrict__ Vo = reinterpret_cast<float*>(ac.v);
+        bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
         const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+        // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
+        // and stored -- element by element, each load waited behind the previous element's stores (the
+        // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
+        // round trips per lane in the epilogue, now TF (one batch of TK x 4 x 3 loads in flight each)
 #pragma unroll
-        for (int i = 0; i < TF; ++i)
+        for (int i = 0; i < TF; ++i) {
+            float pv[TK][4], mv[TK][4], vv[TK][4];
 #pragma unroll
             for (int j = 0; j < TK; ++j) {
                 const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-                if (col >= g.N) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                    if (row < g.M) {
+                    if (col < g.N && row < g.M) {
                         const int64_t e = e0 + (int64_t)row * ldo + col;
-                        float pv = P[e], mv = Mo[e], vv = Vo[e];
-                        adam_elem(pv, mv, vv, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
-                        P[e] = pv; Mo[e] = mv; Vo[e] = vv; Pb[e] = f2bf(pv);
+                        pv[j][r] = P[e];
+                        mv[j][r] = Mo[e];
+                        vv[j][r] = Vo[e];
                     }
                 }
             }
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
+                    if (col < g.N && row < g.M) {
+                        const int64_t e = e0 + (int64_t)row * ldo + col;
+                        float p_ = pv[j][r], m_ = mv[j][r], v_ = vv[j][r];
+                        adam_elem(p_, m_, v_, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
+                        P[e] = p_; Mo[e] = m_; Vo[e] = v_; Pb[e] = f2bf(p_);
+                    }
+                }
+            }
+        }
         return;
     }
 #pragma unroll
