@@ -211,3 +211,23 @@ def test_adam_skip_mask():
         want[e] = True
     bits = np.unpackbits(m[:, None], axis=1, bitorder="little")[:, :4].ravel().astype(bool)
     assert np.array_equal(bits, want)
+
+
+def test_wgrad_row_groups_are_per_problem():
+    """Dense / 1x1 WGRAD: m-split problems get two row groups per block (variant + 500, twice the k-steps
+    per block, half the fixed-point flushes); single-split problems (plain store / fused Adam) keep one.
+    The choice and the split boundaries are functions of the problem alone, whatever shares the launch."""
+    geo = dict(H=1, W=1, OH=1, OW=1, KH=1, KW=1, SH=1, SW=1, a=0, b=0, flags=0)
+    probs = [(60, 16, 300000), (152, 7500, 750), (64, 44, 588000), (150, 300, 75000), (60, 16, 750)]
+    rows = [dict(geo, out=1000 + i, C=N, F=M, M=M, N=N, K=K, adam=1) for i, (M, N, K) in enumerate(probs)]
+    full = {}
+    for v, rws, tiles in H.gemm3_plan(H.MODE_WGRAD, [dict(r) for r in rows], probs):
+        for p, r in enumerate(rws):
+            t = tiles[tiles[:, 0] == p]
+            full[r["out"]] = (v, r["flags"], sorted(set(int(x) for x in t[:, 3])))
+    assert full[1001][0] % 1000 < 500 and full[1001][1] & H.GF_ADAM          # single split: one group, Adam
+    for out in (1000, 1002, 1003):
+        assert full[out][0] % 1000 >= 500 and not full[out][1] & H.GF_WSTORE  # m-split: two groups
+    for r, d in zip(rows, probs):
+        (v, rws, tiles), = H.gemm3_plan(H.MODE_WGRAD, [dict(r)], [d])
+        assert (v, rws[0]["flags"], sorted(set(int(x) for x in tiles[:, 3]))) == full[r["out"]]
