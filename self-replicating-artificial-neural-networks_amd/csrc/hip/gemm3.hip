@@ -29,6 +29,14 @@
 #ifndef WG_NSETS
 #define WG_NSETS 2          // WGRAD register sets in flight (build-time A/B knob)
 #endif
+#ifndef WG_WAVES_PER_EU
+#define WG_WAVES_PER_EU 0   // WGRAD occupancy target (build-time A/B knob; 0: the compiler's choice)
+#endif
+#if WG_WAVES_PER_EU > 0
+#define WG_OCC __attribute__((amdgpu_waves_per_eu(WG_WAVES_PER_EU)))
+#else
+#define WG_OCC
+#endif
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
 // step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
 // in LDS in that layout with 16-B writes; MFMA fragments come from ds_read_b64_tr_b16.
 template <int BMF, int BNK, bool GEN, int NWV = 4, int RG = 1>
-__global__ __launch_bounds__(64 * NWV * RG) void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
+__global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
     constexpr int BKM = 64;
     constexpr int NTH = 64 * NWV;                    // threads per row group (RG row groups per block)
