@@ -646,7 +646,7 @@ def dgrad_reads_natural(KH: int, KW: int, SH: int, SW: int, F: int) -> bool:
     return ("tiled" not in _OFF and "bt" not in _OFF and KH * KW == 1 and SH * SW == 1 and F > BK)
 
 
-SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "48"))   # target k steps per split (0: off)
+SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "32"))   # target k steps per split (0: off; round 2: 48)
 
 
 def tiled_fwd_splits(M: int, N: int, K: int, bn: int, flags: int) -> int:
@@ -704,7 +704,7 @@ CONV_WGRAD_SPLITS = int(_os.environ.get("SERANN_CONV_WGRAD_SPLITS", "64"))
 CONV_WGRAD_MAXPER = int(_os.environ.get("SERANN_CONV_WGRAD_MAXPER", "64"))
 # k' tile width cap: 256 measured 14.56 vs 14.61 ms (4 streams), 18.3 vs 18.6 (1 stream), 12 fewer launches
 CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "256"))
-WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "64"))     # per problem (4-wave blocks)
+WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
