@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-3 GPU session.  STEPS picks the steps (comma list); every GPU step runs under its own time limit and a
+# Round-4 GPU session.  STEPS picks the steps (comma list); every GPU step runs under its own time limit and a
 # step that faults, aborts or times out (rc not 0/1) ends the script.
-#   kernels, engine, rest   the GPU test tiers
+#   tests                   the whole GPU suite in ONE pytest process, exactly as the driver runs it
 #   diag                    per-architecture gradient error report
 #   bench2                  two 1-GPU bench runs whose per-generation records must match (deterministic training)
 #   prof                    rocprofv3 kernel statistics of one bench generation (profiles/r3_kernel_stats.csv)
@@ -29,11 +29,10 @@ stats() {   # keep the kernel statistics of a rocprofv3 run, drop the (large) tr
   f=$(find "$d" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$out"
   find "$d" -name "*_trace.csv" -delete
 }
-STEPS=${STEPS:-kernels,engine,rest,diag,bench2}
+STEPS=${STEPS:-tests,bench1}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
-has kernels && run gpukernels 600 python -u -m pytest tests/test_gpu_kernels.py --maxfail=5 -q --timeout 120 --timeout-method thread
-has engine && run gpuengine 900 python -u -m pytest tests/test_gpu_engine.py --maxfail=5 -v --timeout 300 --timeout-method thread
-has rest && run gpurest 900 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 400 --timeout-method thread --ignore tests/test_gpu_kernels.py --ignore tests/test_gpu_engine.py
+has tests && run gputests 1000 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
+has probe && run probe 60 ./scripts/micro/rsrc_probe
 has diag && run diag 600 python -u scripts/diag_grad_err.py
 if has bench2; then
   run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1

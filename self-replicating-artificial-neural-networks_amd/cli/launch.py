@@ -8,10 +8,14 @@ run is SPMD over ``torch.distributed``: either launched by ``torch.distributed.r
 
 Recovery: with ``--max-restarts N`` the launcher supervises the run as a child process
 (``torch.distributed.run`` for ``--nproc > 1``, the script itself otherwise).  Rank 0 records the
-experiment id in ``SERANN_RUN_ID_FILE`` as soon as it is known; when the child fails -- a crashed rank,
-or a rank's generation watchdog (``worker_pool_job_timeout``, utils/faults.py) -- the launcher relaunches
-it with ``--resume-experiment-id <id>``, which continues from the last committed generation (exactly,
-through the ``resume_state`` table), up to N times.
+experiment id in ``SERANN_RUN_ID_FILE`` once the run's ``execution_info`` row is saved, and the number
+of the last committed generation after each generation; when the child fails -- a crashed rank, or a
+rank's generation watchdog (``worker_pool_job_timeout``, utils/faults.py) -- the launcher relaunches it
+with ``--resume-experiment-id <id>``, which continues from the last committed generation (exactly,
+through the ``resume_state`` table), up to N times.  A relaunch is marked ``SERANN_SUPERVISED_RESUME=1``
+(it never extends ``num_generations`` the way a manual resume of a finished run does), and the
+supervisor gives up when the watchdog fires twice at the same committed generation: the same work
+would only time out again.
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ from typing import List, Optional
 
 RUN_ID_ENV = "SERANN_RUN_ID_FILE"
 CHILD_ENV = "SERANN_LAUNCH_CHILD"
+RESUME_ENV = "SERANN_SUPERVISED_RESUME"
 
 
 def add_pool_args(parser):
@@ -37,12 +42,28 @@ def add_pool_args(parser):
                         help="relaunch a failed run up to N times, resuming from the last committed generation")
 
 
-def record_run_id(experiment_id: str) -> None:
-    """Rank 0: publish the experiment id for the supervising launcher (no-op when unsupervised)."""
+def record_run_id(experiment_id: str, committed_generation: Optional[int] = None) -> None:
+    """Rank 0: publish the experiment id (and the last committed generation) for the supervising
+    launcher (no-op when unsupervised).  Call it only once the run is resumable: after its
+    ``execution_info`` row exists."""
     path = os.environ.get(RUN_ID_ENV)
     if path:
-        with open(path, "w") as f:
-            f.write(str(experiment_id))
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(str(experiment_id) + ("" if committed_generation is None else f"\n{int(committed_generation)}"))
+        os.replace(tmp, path)
+
+
+def read_run_id(path: str):
+    """(experiment id or "", last committed generation or None) from a run-id file."""
+    try:
+        with open(path) as f:
+            parts = f.read().split()
+    except FileNotFoundError:
+        return "", None
+    if not parts:
+        return "", None
+    return parts[0], (int(parts[1]) if len(parts) > 1 else None)
 
 
 def _with_resume(argv: List[str], experiment_id: str) -> List[str]:
@@ -71,6 +92,8 @@ def supervise(cmd_for, argv: List[str], max_restarts: int, env: Optional[dict] =
     env[RUN_ID_ENV] = id_file
     env[CHILD_ENV] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    from ..utils.faults import EXIT_TIMEOUT
+    timed_out_at = None
     try:
         attempt = 0
         while True:
@@ -82,18 +105,26 @@ def supervise(cmd_for, argv: List[str], max_restarts: int, env: Optional[dict] =
                 print(f"[launch] run failed with status {rc}; restart {attempt}/{max_restarts}", file=sys.stderr,
                       flush=True)
                 continue
-            with open(id_file) as f:
-                run_id = f.read().strip()
+            run_id, committed = read_run_id(id_file)
             if not run_id:
-                print(f"[launch] run failed (status {rc}) before an experiment id was recorded; not restarting",
+                print(f"[launch] run failed (status {rc}) before the experiment was resumable; not restarting",
                       file=sys.stderr, flush=True)
                 return rc
+            if rc == EXIT_TIMEOUT:
+                if timed_out_at is not None and timed_out_at == committed:
+                    print(f"[launch] the generation watchdog fired again after committed generation {committed}; "
+                          f"the same work would time out again: not restarting", file=sys.stderr, flush=True)
+                    return rc
+                timed_out_at = committed
             attempt += 1
             print(f"[launch] run failed with status {rc}; restart {attempt}/{max_restarts}: resuming experiment "
                   f"{run_id}", file=sys.stderr, flush=True)
             argv = _with_resume(argv, run_id)
+            env[RESUME_ENV] = "1"
     finally:
-        os.unlink(id_file)
+        for f_ in (id_file, id_file + ".tmp"):
+            if os.path.exists(f_):
+                os.unlink(f_)
 
 
 def maybe_relaunch(args, script: str, argv: Optional[List[str]] = None, resume: bool = True) -> None:

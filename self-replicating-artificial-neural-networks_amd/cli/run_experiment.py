@@ -36,7 +36,7 @@ def get_args(argv=None):
 
 def main(argv=None, script=None):
     args = get_args(argv)
-    from .launch import maybe_relaunch, record_run_id
+    from .launch import RESUME_ENV, maybe_relaunch, record_run_id
     maybe_relaunch(args, script or str(Path(__file__).resolve().parents[2] / "evolutionary_experiment" /
                                        "run_experiment.py"), argv)
 
@@ -78,7 +78,9 @@ def main(argv=None, script=None):
                 parameters = {k: v for k, v in info.drop("start_time").items()}
                 for k in ("host_name", "encodings_dataset", "tokens_vocabulary", "ribosomal_autoencoder", "random_seed"):
                     parameters.pop(k, None)
-                if start_generation == parameters["num_generations"]:
+                # a manual resume of a finished run extends it (reference run_experiment.py:93-95); a
+                # supervised relaunch after the last generation must not run a second set
+                if start_generation == parameters["num_generations"] and not os.environ.get(RESUME_ENV):
                     parameters["num_generations"] *= 2
             state = (start_generation, parameters, stored_seed)
         start_generation, parameters, stored_seed = comm.broadcast_object(state)
@@ -98,13 +100,17 @@ def main(argv=None, script=None):
     parameters["ribosomal_autoencoder"] = s.codec.get_model_name()
     parameters["random_seed"] = seed
     if comm.is_root:
-        record_run_id(experiment_id)
         print(f"Experiment id: {experiment_id} | ranks: {comm.world_size} | engine: {s.engine} | "
               f"codec: {s.codec.get_model_name()} | data: {'synthetic' if s.data.synthetic else 'MNIST'}", flush=True)
     exp = Experiment(experiment_id, s.encodings, s.worker, db, parameters, s.codec, comm=comm,
                      start_generation=start_generation, random_seed=seed, strict_reference=args.strict_reference,
                      perf_log=args.perf_log)
-    exp.execute(max_generations=args.max_generations)
+    if comm.is_root:
+        # resumable from here on (execution_info is saved): tell a supervising launcher, then keep it told
+        # which generation was committed last
+        record_run_id(experiment_id, start_generation - 1 if start_generation > 0 else None)
+    exp.execute(max_generations=args.max_generations,
+                on_generation=(lambda g, rec: record_run_id(experiment_id, g)) if comm.is_root else None)
     comm.shutdown()
     return experiment_id
 

@@ -1,7 +1,7 @@
 // Auxiliary grouped kernels for the SeRANN population engine:
 //   gather_batch (K14), DGRAD weight transposes, fused BatchNormalizationF16
 //   train/infer/backward (K05/K06), maxpool fwd/bwd (K03), concat copies (K08), fused heads loss
-//   (softmax-CE + sigmoid-MSE + accuracy + dlogits, K10/K11/K12/K17), popstats (K20-K22).
+//   (softmax-CE + sigmoid-MSE + accuracy + dlogits, K10/K11/K12/K17).
 // Grouped kernels take a descriptor array and an int2 tile table (problem, chunk).
 #include <hip/hip_fp16.h>
 #include "common.h"
@@ -717,32 +717,6 @@ __global__ __launch_bounds__(256) void loss_kernel(const LossDesc* __restrict__ 
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Pairwise genotype statistics over bit-packed genotypes: sum_{i<j} hamming, sum_{i<j} sqrt(hamming).
-__global__ __launch_bounds__(256) void popstats_kernel(const uint64_t* __restrict__ bits, int n, int words,
-                                                       double* __restrict__ out) {
-    const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
-    if (j0 + 63 < i0) return;
-    double sh = 0.0, se = 0.0;
-    for (int p = threadIdx.x; p < 64 * 64; p += blockDim.x) {
-        const int i = i0 + p / 64, j = j0 + p % 64;
-        if (i >= n || j >= n || j <= i) continue;
-        int dsum = 0;
-        for (int w = 0; w < words; ++w) dsum += __popcll(bits[(int64_t)i * words + w] ^ bits[(int64_t)j * words + w]);
-        sh += dsum;
-        se += sqrt((double)dsum);
-    }
-    // wave reduce then one atomic per wave
-    for (int o = 32; o > 0; o >>= 1) {
-        sh += __shfl_xor(sh, o, 64);
-        se += __shfl_xor(se, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&out[0], sh);
-        atomicAdd(&out[1], se);
-    }
-}
-
 // ================================================================================================
 void launch_gather_batch(uint64_t x_all, uint64_t g_all, uint64_t y_all, uint64_t perm, uint64_t counter,
                          int64_t base, int64_t B, int64_t n_perm, int64_t x_cols, int64_t g_cols,
@@ -808,14 +782,6 @@ void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t s
     dim3 grid((unsigned)((B + LOSS_ROWS - 1) / LOSS_ROWS), (unsigned)nprob);
     hipLaunchKernelGGL(loss_kernel, grid, dim3(256), 0, as_stream(stream), as_ptr<const LossDesc>(descs), train,
                        (int)nvalid);
-    SERANN_CHECK(hipGetLastError());
-}
-
-void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream) {
-    if (n < 2) return;
-    const unsigned t = (unsigned)((n + 63) / 64);
-    hipLaunchKernelGGL(popstats_kernel, dim3(t, t), dim3(256), 0, as_stream(stream), as_ptr<const uint64_t>(bits),
-                       (int)n, (int)words, as_ptr<double>(partials));
     SERANN_CHECK(hipGetLastError());
 }
 

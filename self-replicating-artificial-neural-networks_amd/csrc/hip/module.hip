@@ -44,7 +44,6 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("gchain", &launch_gchain);
     m.def("copy2d", &launch_copy2d);
     m.def("loss", &launch_loss);
-    m.def("popstats", &launch_popstats);
     m.def("memset32", &launch_memset32);
     m.def("group_argmax", &launch_group_argmax);
     m.def("imcol", &launch_imcol);

@@ -61,7 +61,6 @@ void launch_bn(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64
 void launch_pool(int backward, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid);
-void launch_popstats(uint64_t bits, int64_t n, int64_t words, uint64_t partials, uint64_t stream);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
 void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_concrete_fwd(uint64_t logits, uint64_t u, uint64_t s, uint64_t z, uint64_t kl, int64_t B, int64_t G,

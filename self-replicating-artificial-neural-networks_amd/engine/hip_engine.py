@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -183,15 +184,43 @@ class Arena:
         return self.t.data_ptr() + off * self.t.element_size()
 
 
-_DEVICE_DATA: Dict[Tuple[int, str], dict] = {}
+# Device copies of the shared training / test arrays, owned by their source objects: a weak-keyed map
+# from the host object to its uploads, so an upload lives exactly as long as the dataset (or test array)
+# it mirrors -- no process-lifetime device cache, no id() reuse hazard.
+class _UploadCache:
+    """Identity-keyed map host object -> {device: uploads} that holds its keys weakly (numpy arrays and
+    dataclasses are unhashable, so WeakKeyDictionary does not apply): an entry dies with its key."""
+
+    def __init__(self):
+        self._d: Dict[int, tuple] = {}
+
+    def setdefault(self, key, default):
+        k = id(key)
+        ent = self._d.get(k)
+        if ent is not None and ent[0]() is key:
+            return ent[1]
+
+        def _drop(_ref, k=k):
+            cur = self._d.get(k)
+            if cur is not None and cur[0] is _ref:
+                del self._d[k]
+        self._d[k] = (weakref.ref(key, _drop), default)
+        return default
+
+    def clear(self):
+        self._d.clear()
+
+    def __len__(self):
+        return len(self._d)
+
+
+_DEVICE_DATA = _UploadCache()
 
 
 def device_data(data, device) -> dict:
-    """Upload the (shared) training/test arrays once per process, as bf16 / int32."""
-    key = (id(data), str(device))
-    d = _DEVICE_DATA.get(key)
-    if d is not None and d.get("_src") is not data:
-        d = None          # id() reused by a different object: never serve a stale (wrongly shaped) upload
+    """Upload the (shared) training/test arrays once per dataset object and device, as bf16 / int32."""
+    per_dev = _DEVICE_DATA.setdefault(data, {})
+    d = per_dev.get(str(device))
     if d is None:
         def bf(a):
             return torch.as_tensor(np.ascontiguousarray(a.reshape(len(a), -1)), dtype=torch.float32).to(
@@ -202,10 +231,14 @@ def device_data(data, device) -> dict:
             "train_y": torch.as_tensor(data.train_labels.astype(np.int32), device=device),
             "test_x": bf(data.test_x), "test_g": bf(data.test_g),
             "test_y": torch.as_tensor(data.test_labels.astype(np.int32), device=device),
-            "_src": data,
         }
-        _DEVICE_DATA[key] = d
+        per_dev[str(device)] = d
     return d
+
+
+def release_device_data() -> None:
+    """Drop every cached upload (the OOM path frees them before a retry)."""
+    _DEVICE_DATA.clear()
 
 
 # ------------------------------------------------------------------------------------------------
@@ -285,6 +318,9 @@ class HipPopulationEngine(PopulationEngine):
         self.plans: Dict[tuple, Plan] = {}
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.timings: Dict[str, float] = {}
+        # raw input buffers by device address (the torch fallbacks of rare ops view them); entries are only
+        # ever added -- every plan keeps its buffers alive, so an address cannot be reused while listed
+        self._input_tensors: Dict[int, torch.Tensor] = {}
 
     # ---------------------------------------------------------------------------------------------
     # parameters
@@ -1474,7 +1510,7 @@ class HipPopulationEngine(PopulationEngine):
         xb = _padded_zeros((B, xcols), torch.bfloat16, dev)
         gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
         yb = torch.zeros(B, dtype=torch.int32, device=dev)
-        self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
+        self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
         perm_t = torch.zeros(max(split, 1), dtype=torch.int32, device=dev)
         counter = torch.zeros(1, dtype=torch.int32, device=dev)
         metrics = torch.zeros(P, 4, dtype=torch.int64, device=dev)      # Q32 fixed point (aux.hip loss_kernel)
@@ -1637,10 +1673,11 @@ class HipPopulationEngine(PopulationEngine):
         metrics).  Used by the numerics tests against the torch oracle."""
         dev = self.device
         B = len(x)
-        xb = torch.as_tensor(np.ascontiguousarray(x.reshape(B, -1)), dtype=torch.float32, device=dev).to(torch.bfloat16)
-        gb = torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32, device=dev).to(torch.bfloat16)
-        yb = torch.as_tensor(y.astype(np.int32), device=dev)
-        self._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
+        # kernel operands keep the fragment-load slack behind them (hip_ops.operand)
+        xb = H.padded(torch.as_tensor(np.ascontiguousarray(x.reshape(B, -1)), dtype=torch.float32, device=dev).to(torch.bfloat16))
+        gb = H.padded(torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32, device=dev).to(torch.bfloat16))
+        yb = H.padded(torch.as_tensor(y.astype(np.int32), device=dev))
+        self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
         metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
         mem = self._alloc_buffers(B, with_grads=True)
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
@@ -1685,7 +1722,6 @@ class HipPopulationEngine(PopulationEngine):
             gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
             yb = torch.zeros(B, dtype=torch.int32, device=dev)
             metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
-            self._input_tensors = getattr(self, "_input_tensors", {})
             self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
             mem = getattr(self, "_train_mem", None)
             if mem is None or mem["B"] != B:
@@ -1733,7 +1769,6 @@ class HipPopulationEngine(PopulationEngine):
             L = self.layouts[0].ir.genotype_size
             xs = _padded_zeros((P, B, xcols), torch.bfloat16, dev)
             gs = _padded_zeros((P, B, L), torch.bfloat16, dev)
-            self._input_tensors = getattr(self, "_input_tensors", {})
             for i in range(P):
                 self._input_tensors[xs[i].data_ptr()] = xs[i]
                 self._input_tensors[gs[i].data_ptr()] = gs[i]
@@ -1802,19 +1837,31 @@ class HipPopulationEngine(PopulationEngine):
         return self._replicate_chunks(genotypes, images, cfg, packed=True)
 
     def close(self):
+        """Release every device resource the engine owns besides its parameters: the captured graph first
+        (its replay addresses the buffers below), then plans, activation / gradient buffers, descriptor
+        tables and side streams.  Waits for the device first, so nothing in flight still reads them."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         self.graph = None
         self.plans.clear()
+        for name in ("_train_mem", "_train_mem_rem", "_debug_mem", "_adam_skip", "_adam_ctx", "_streams"):
+            if hasattr(self, name):
+                delattr(self, name)
+        self._input_tensors = {}
 
 
 def device_data_for_arrays(x, labels, g, device):
-    key = ("eval", id(x), id(labels), id(g), str(device))
-    d = _DEVICE_DATA.get(key)
-    if d is not None and not (d["_src"][0] is x and d["_src"][1] is labels and d["_src"][2] is g):
-        d = None          # ids reused by other arrays: re-upload
+    """Upload an evaluation set (x, labels, g) once per x array and device (weak-keyed on x: freed with
+    it); labels / g are matched by identity through weak references."""
+    per_x = _DEVICE_DATA.setdefault(x, {})
+    d = per_x.get(str(device))
+    if d is not None and not (d["_labels"]() is labels and d["_g"]() is g):
+        d = None
     if d is None:
         d = {"x": torch.as_tensor(np.ascontiguousarray(x.reshape(len(x), -1)), dtype=torch.float32).to(device).to(
             torch.bfloat16),
              "g": torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32).to(device).to(torch.bfloat16),
-             "y": torch.as_tensor(labels.astype(np.int32), device=device), "_src": (x, labels, g)}
-        _DEVICE_DATA[key] = d
+             "y": torch.as_tensor(labels.astype(np.int32), device=device),
+             "_labels": weakref.ref(labels), "_g": weakref.ref(g)}
+        per_x[str(device)] = d
     return d

@@ -34,7 +34,7 @@ import pandas as pd
 from ..genome.interpreter import layer_counts
 from ..parallel.comm import Comm, LocalComm, pack_header, unpack_results
 from ..parallel.partition import lpt_partition
-from ..utils.faults import GenerationWatchdog, maybe_inject
+from ..utils.faults import GenerationWatchdog, job_scale, maybe_inject
 from ..utils.levenshtein import levenshtein_batch
 from ..utils.stats import fertility, genotype_stats, source_code_stats
 from ..utils.trace import PhaseTimer, phase
@@ -73,9 +73,16 @@ class Experiment:
                                      int(parameters["num_classification_classes"]))
         self.history: List[dict] = []
         if job_timeout is None:
+            # the reference pool's per-job timeout (config.py:7), armed by default only where a stall is
+            # plausible and recoverable: the GPU engine, or a run under the supervising launcher.  A slow
+            # but healthy CPU run is never killed by it.
+            from ..cli.launch import CHILD_ENV
             from ..config import experiment_config
-            job_timeout = float(experiment_config["worker_pool_job_timeout"])
-        # per-generation job timeout (the reference pool's worker_pool_job_timeout, config.py:7)
+            import os
+            gpu = str(getattr(worker, "engine_name", "")) == "hip"
+            job_timeout = float(experiment_config["worker_pool_job_timeout"]) if (gpu or os.environ.get(CHILD_ENV)) \
+                else 0.0
+        # per-generation watchdog, scaled to the rank's shard once the partition is known
         self._watchdog = GenerationWatchdog(job_timeout, self._comm.rank)
         if self._comm.is_root and self._db is not None:
             self._db.save_execution_info(datetime.now(), self._parameters)
@@ -248,6 +255,8 @@ class Experiment:
         plan = plan_generation(sources, self._cache, float(p["max_serann_parameters"]), comm)
         parts = lpt_partition(plan.costs, comm.world_size, plan.arch_keys)
         local = [int(plan.trainable[i]) for i in parts[comm.rank]]
+        # the shard is this many reference pool jobs: give the watchdog that many job timeouts
+        self._watchdog.arm(f"generation {generation}", job_scale(len(local)))
         ids = list(current.index)
         genotypes = np.stack([np.asarray(g, np.float64) for g in current["genotype"]])
         position = {int(t): k for k, t in enumerate(plan.trainable)}

@@ -309,6 +309,37 @@ def check_layouts():
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
 
+OPERAND_SLACK_BYTES = 256   # readable memory every kernel operand must have behind its last element
+
+
+def operand(shape, dtype, device, zero: bool = True):
+    """A kernel operand of ``shape``: contiguous, followed by OPERAND_SLACK_BYTES of zeroed memory.
+
+    Contract of every gemm3 / conv / BN kernel: a 16-B fragment load may start at any valid element,
+    so up to 14 bytes past an operand's last element are read (the over-read lanes are masked, never
+    used).  Plain ``torch.empty`` tensors can end at the last mapped byte of an allocator segment, where
+    that read faults the GPU; every buffer handed to these kernels comes from here (or an engine arena,
+    which keeps the same slack)."""
+    import torch
+    shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list, torch.Size)) else (shape,)))
+    n = 1
+    for s in shape:
+        n *= s
+    esz = torch.empty(0, dtype=dtype).element_size()
+    extra = -(-OPERAND_SLACK_BYTES // esz)
+    buf = (torch.zeros if zero else torch.empty)(n + extra, dtype=dtype, device=device)
+    if not zero:
+        buf[n:].zero_()
+    return buf[:n].view(shape)
+
+
+def padded(t):
+    """``t``'s values as a kernel operand (see :func:`operand`)."""
+    out = operand(t.shape, t.dtype, t.device, zero=False)
+    out.copy_(t)
+    return out
+
+
 def stream_handle():
     import torch
     return torch.cuda.current_stream().cuda_stream

@@ -51,10 +51,11 @@ class HipRiboDecoder:
             s2f = s2.repeat(L)
             w2 = wd * s2f[:, None]
             b2 = gn.dense.bias * s2f + t2.repeat(L)
-            self.w1 = w1.to(self.device, torch.bfloat16).contiguous()
-            self.b1 = b1.to(self.device, torch.float32).contiguous()
-            self.w2 = w2.to(self.device, torch.bfloat16).contiguous()
-            self.b2 = b2.to(self.device, torch.float32).contiguous()
+            # kernel operands carry the fragment-load slack (hip_ops.operand)
+            self.w1 = H.padded(w1.to(self.device, torch.bfloat16).contiguous())
+            self.b1 = H.padded(b1.to(self.device, torch.float32).contiguous())
+            self.w2 = H.padded(w2.to(self.device, torch.bfloat16).contiguous())
+            self.b2 = H.padded(b2.to(self.device, torch.float32).contiguous())
             # fp32 copies for the near-tie rescoring (``_rescore``)
             self.w1f = (w * s1[:, None, None]).to(self.device, torch.float32).contiguous()   # (32, A, 5)
             self.b1f = b1.to(self.device, torch.float32).contiguous()
@@ -72,10 +73,10 @@ class HipRiboDecoder:
             return self._plans[B]
         G, A, V, L, C1 = self.G, self.A, self.V, self.L, self.C1
         OL, dev = G - 4, self.device
-        x = torch.zeros(B * G * A + 64, dtype=torch.bfloat16, device=dev)
-        h = torch.zeros(B * OL * C1 + 64, dtype=torch.bfloat16, device=dev)
-        logits = torch.empty(B, L * V, dtype=torch.float32, device=dev)
-        out = torch.empty(B, L, dtype=torch.int32, device=dev)
+        x = H.operand(B * G * A, torch.bfloat16, dev)
+        h = H.operand(B * OL * C1, torch.bfloat16, dev)
+        logits = H.operand((B, L * V), torch.float32, dev)
+        out = H.operand((B, L), torch.int32, dev)
         K1, K2 = 5 * A, OL * C1
         launches = []
         for row, dims in ((dict(a=x.data_ptr(), b=self.w1.data_ptr(), out=h.data_ptr(), bias=self.b1.data_ptr(),
@@ -167,16 +168,16 @@ class HipRiboEncoder:
             s0, t0 = _fold_bn(net.bn0)
             table = net.embedding.weight * s0[0] + t0[0]                    # (V, E)
             self.V = table.shape[0]
-            self.table = table.to(self.device, torch.bfloat16).contiguous()
+            self.table = H.padded(table.to(self.device, torch.bfloat16).contiguous())
             self.convs = []
             for conv, bn in ((net.conv1, net.bn1), (net.conv2, net.bn2), (net.conv3, net.bn3)):
                 sc, sh = _fold_bn(bn)
                 w = (conv.weight * sc[:, None, None, None]).permute(0, 2, 3, 1).contiguous()  # [F][KH][KW][C]
                 b = conv.bias * sc + sh
-                self.convs.append((w.to(self.device, torch.bfloat16).contiguous(),
-                                   b.to(self.device, torch.float32).contiguous(), conv.kernel_size))
-            self.wd = net.dense.weight.to(self.device, torch.bfloat16).contiguous()          # [N][K]
-            self.bd = net.dense.bias.to(self.device, torch.float32).contiguous()
+                self.convs.append((H.padded(w.to(self.device, torch.bfloat16).contiguous()),
+                                   H.padded(b.to(self.device, torch.float32).contiguous()), conv.kernel_size))
+            self.wd = H.padded(net.dense.weight.to(self.device, torch.bfloat16).contiguous())          # [N][K]
+            self.bd = H.padded(net.dense.bias.to(self.device, torch.float32).contiguous())
         self._plans = {}
 
     def stale(self, model) -> bool:
@@ -188,13 +189,13 @@ class HipRiboEncoder:
             return self._plans[B]
         dev = self.device
         Hh, Ww, C = self.L, self.E, 1
-        x = torch.empty(B, Hh, Ww, C, dtype=torch.bfloat16, device=dev)
+        x = H.operand((B, Hh, Ww, C), torch.bfloat16, dev)
         bufs, launches = [x], []
         cur = x
         for w, b, (kh, kw) in self.convs:
             F = w.shape[0]
             OH, OW = Hh - kh + 1, Ww - kw + 1
-            y = torch.empty(B, OH, OW, F, dtype=torch.bfloat16, device=dev)
+            y = H.operand((B, OH, OW, F), torch.bfloat16, dev)
             K = kh * kw * C
             row = dict(a=cur.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=Hh, W=Ww, C=C,
                        OH=OH, OW=OW, F=F, KH=kh, KW=kw, SH=1, SW=1, M=B * OH * OW, N=F, K=K, act=0,
@@ -208,13 +209,13 @@ class HipRiboEncoder:
             cur, Hh, Ww, C = y, OH, OW, F
         K = Hh * Ww * C
         N = self.G * self.A
-        logits = torch.zeros(B, N, dtype=torch.float32, device=dev)
+        logits = H.operand((B, N), torch.float32, dev)
         kt = -(-K // H.BK)
         per = self.SPLIT_KSTEPS
         ns = -(-kt // per)
         # split-K: split s writes its fp32 partial tile to ws[s] (GF_SPLITWS); splitk_finalize sums the
         # splits in order and adds the bias (deterministic, no atomics)
-        ws = torch.empty(ns * B * N, dtype=torch.float32, device=dev)
+        ws = H.operand(ns * B * N, torch.float32, dev)
         row = dict(a=cur.data_ptr(), b=self.wd.data_ptr(), out=logits.data_ptr(), bias=0, aux=ws.data_ptr(),
                    H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1, M=B, N=N, K=K, act=0, kper=per, sbase=0,
                    flags=H.GF_SPLITWS | (H.GF_VEC_A | H.GF_VEC_B if K % 8 == 0 else 0))
@@ -232,7 +233,7 @@ class HipRiboEncoder:
         ft = torch.as_tensor(H.chunk_tiles([B * N], H.SPLITFIN_ELEMS), device=dev)
         bufs.append(ws)
         dense = (7128, d, t, fd, ft)
-        bits = torch.empty(B * self.G, dtype=torch.int32, device=dev)
+        bits = H.operand(B * self.G, torch.int32, dev)
         plan = dict(x=x, bufs=bufs, convs=launches, dense=dense, logits=logits, bits=bits)
         self._plans[B] = plan
         return plan

@@ -449,16 +449,52 @@ class HipRiboTrainer:
         return {"loss": nelbo, "nll": -logpx.mean(), "kld": kl.mean()}
 
     # checkpoint interface of the trainer's optimizer (riboae/trainer.py saves ``opt.state_dict()``)
+    def _moment_views(self, arena: torch.Tensor) -> List[torch.Tensor]:
+        """Torch-layout views of ``arena`` (an Adam moment arena) in ``model.parameters()`` order -- the
+        per-parameter list format of the torch engine's optimizer (ScheduledKerasAdam.state_dict)."""
+        where = {}
+        for name, mod, attr, klayout, perm in self.specs:
+            off, cnt = self.pa.items[name]
+            flat = arena.narrow(0, off, cnt)
+            where[id(getattr(mod, attr))] = flat.view(getattr(mod, attr).shape) if klayout is None else \
+                flat.view(klayout).permute(*perm)
+        out = []
+        for p in self.model.parameters():
+            if id(p) not in where:
+                raise RuntimeError("model parameter outside the HIP trainer's arena")
+            out.append(where[id(p)])
+        return out
+
     def state_dict(self):
+        """Both layouts: the flat arenas (exact, fast resume on this engine) and per-parameter lists in
+        ``model.parameters()`` order, so a HIP checkpoint resumes on the torch engine too."""
         n = self.pa.size
-        return {"t": int(self.step_i.item()), "m_arena": self.m[:n].detach().cpu(), "v_arena": self.v[:n].detach().cpu()}
+        return {"t": int(self.step_i.item()), "m_arena": self.m[:n].detach().cpu(), "v_arena": self.v[:n].detach().cpu(),
+                "m": [v.detach().cpu().contiguous() for v in self._moment_views(self.m)],
+                "v": [v.detach().cpu().contiguous() for v in self._moment_views(self.v)]}
 
     def load_state_dict(self, st):
+        """Accepts this engine's arenas or the torch engine's per-parameter moment lists.  A state with
+        neither restarts Adam from scratch (t = 0 with zero moments: keeping a large t over zero moments
+        would skew the bias correction and inflate the first updates)."""
         n = self.pa.size
-        if "m_arena" in st:
-            self.m[:n].copy_(st["m_arena"].to(self.dev))
-            self.v[:n].copy_(st["v_arena"].to(self.dev))
-        self.step_i.fill_(int(st["t"]))
+        t = int(st.get("t", 0))
+        with torch.no_grad():
+            if "m_arena" in st:
+                self.m[:n].copy_(st["m_arena"].to(self.dev))
+                self.v[:n].copy_(st["v_arena"].to(self.dev))
+            elif "m" in st and "v" in st:
+                for arena, key in ((self.m, "m"), (self.v, "v")):
+                    views = self._moment_views(arena)
+                    if len(views) != len(st[key]):
+                        raise ValueError(f"optimizer state has {len(st[key])} moments, model has {len(views)}")
+                    for dst, src in zip(views, st[key]):
+                        dst.copy_(src.to(self.dev).reshape(dst.shape))
+            else:
+                self.m.zero_()
+                self.v.zero_()
+                t = 0
+        self.step_i.fill_(t)
 
     def debug_grads(self, tokens, temperature, kld_weight, noise):
         """Gradients of one step without the Adam update (numerics tests): {param name: torch-layout

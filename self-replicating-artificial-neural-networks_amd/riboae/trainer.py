@@ -62,11 +62,22 @@ class ScheduledKerasAdam(KerasAdam):
         return {"t": self.t, "m": [m.detach().cpu() for m in self.m], "v": [v.detach().cpu() for v in self.v]}
 
     def load_state_dict(self, st):
+        """Accepts this optimizer's per-parameter lists (also written by the HIP trainer next to its
+        arenas).  Arena-only states from older HIP checkpoints cannot be mapped without the HIP trainer:
+        Adam then restarts from t = 0 with zero moments instead of mixing a large t with fresh moments."""
+        if "m" not in st or "v" not in st:
+            self.t = 0
+            for buf in list(self.m) + list(self.v):
+                buf.zero_()
+            return
+        if len(st["m"]) != len(self.m):
+            raise ValueError(f"optimizer state has {len(st['m'])} moments, model has {len(self.m)}")
         self.t = int(st["t"])
-        for dst, src in zip(self.m, st["m"]):
-            dst.copy_(src)
-        for dst, src in zip(self.v, st["v"]):
-            dst.copy_(src)
+        with torch.no_grad():
+            for dst, src in zip(self.m, st["m"]):
+                dst.copy_(src.to(dst.device).reshape(dst.shape))
+            for dst, src in zip(self.v, st["v"]):
+                dst.copy_(src.to(dst.device).reshape(dst.shape))
 
 
 def get_dataset(sequences: np.ndarray, train_test_ratio: float):
@@ -105,11 +116,7 @@ def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out
     else:
         opt = ScheduledKerasAdam(list(model.parameters()), lr=learning_rate_at(1), eps=1e-7)
     if ck is not None and ck.get("optimizer"):
-        st = ck["optimizer"]
-        if hip is None or "m_arena" in st:
-            opt.load_state_dict(st)
-        else:
-            hip.step_i.fill_(int(st["t"]))                     # a torch-path checkpoint: keep its step count
+        opt.load_state_dict(ck["optimizer"])                    # either engine reads either format
     if bf16 is None:
         bf16 = dev.type == "cuda"
     data = torch.as_tensor(np.asarray(train_tokens), dtype=torch.long)

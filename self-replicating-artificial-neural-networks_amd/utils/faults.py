@@ -67,6 +67,14 @@ def maybe_inject(generation: int, rank: int = 0, spec: Optional[str] = None) -> 
     raise InjectedFault(f"injected fault: rank {rank} at generation {generation}")
 
 
+JOB_ORGANISMS = 112      # organisms per pool job in the reference split (logic/experiment.py:170-178)
+
+
+def job_scale(n_organisms: int, waves: int = 1) -> float:
+    """How many reference pool jobs a shard of ``n_organisms`` (trained in ``waves`` sequential waves) is."""
+    return float(max(1, -(-int(n_organisms) // JOB_ORGANISMS), int(waves)))
+
+
 class GenerationWatchdog:
     """Arms a timer for the work of one generation; if it is not disarmed within ``timeout_s`` the
     process reports the stall on stderr and exits with ``EXIT_TIMEOUT`` (``os._exit``: a stalled device
@@ -78,20 +86,25 @@ class GenerationWatchdog:
         self.exit_status = int(exit_status)
         self._timer: Optional[threading.Timer] = None
         self._label = ""
+        self._armed_s = self.timeout_s
 
     def _fire(self):
-        sys.stderr.write(f"[watchdog] rank {self.rank}: {self._label} exceeded the job timeout of "
-                         f"{self.timeout_s:.0f} s (worker_pool_job_timeout); exiting with status "
+        sys.stderr.write(f"[watchdog] rank {self.rank}: {self._label} exceeded its timeout of "
+                         f"{self._armed_s:.0f} s (worker_pool_job_timeout per job); exiting with status "
                          f"{self.exit_status} for a relaunch with --resume-experiment-id\n")
         sys.stderr.flush()
         sys.stdout.flush()
         os._exit(self.exit_status)
 
-    def arm(self, label: str = "generation") -> "GenerationWatchdog":
+    def arm(self, label: str = "generation", scale: float = 1.0) -> "GenerationWatchdog":
+        """(Re-)arm for ``scale`` x ``timeout_s``: the reference's timeout bounded one pool job of at most
+        ``JOB_ORGANISMS`` organisms, so a rank's shard of n organisms gets ceil(n / JOB_ORGANISMS) jobs'
+        worth (:func:`job_scale`)."""
         self.disarm()
         self._label = label
+        self._armed_s = self.timeout_s * max(1.0, float(scale))
         if self.timeout_s > 0:
-            self._timer = threading.Timer(self.timeout_s, self._fire)
+            self._timer = threading.Timer(self._armed_s, self._fire)
             self._timer.daemon = True
             self._timer.start()
         return self

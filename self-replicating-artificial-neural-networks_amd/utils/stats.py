@@ -9,7 +9,7 @@ Definitions kept exactly:
 * ``species_richness`` = number of distinct genotypes (sources).
 
 Genotypes are {0,1}, so Euclidean = sqrt(Hamming count): one popcount pass over bit-packed
-genotypes (native C++ or the HIP ``popstats`` kernel) replaces the reference's ~1.5 M Python
+genotypes (native C++, ``csrc/host/serann_host_core.h``) replaces the reference's ~1.5 M Python
 callbacks per generation at pop=1000.
 """
 from __future__ import annotations

@@ -125,7 +125,7 @@ def test_watchdog_fires_on_a_stalled_generation(tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=60)
     from serann.utils.faults import EXIT_TIMEOUT
     assert r.returncode == EXIT_TIMEOUT, (r.returncode, r.stderr)
-    assert "exceeded the job timeout" in r.stderr
+    assert "exceeded its timeout" in r.stderr
     assert time.time() - t0 < 30
 
 
@@ -162,6 +162,55 @@ def test_supervised_relaunch_resumes_with_recorded_id(tmp_path):
     bad = tmp_path / "bad.py"
     bad.write_text("import sys; sys.exit(3)\n")
     assert supervise(lambda a: [sys.executable, str(bad), *a], [], max_restarts=3) == 3
+
+
+def test_supervisor_stops_when_watchdog_repeats_at_same_generation(tmp_path):
+    """A watchdog timeout (EXIT_TIMEOUT) at the same committed generation twice ends supervision: the
+    relaunch would redo the identical work.  Relaunches carry SERANN_SUPERVISED_RESUME=1."""
+    from serann.cli.launch import RESUME_ENV, RUN_ID_ENV, read_run_id, record_run_id, supervise
+    from serann.utils.faults import EXIT_TIMEOUT
+    log = tmp_path / "calls.txt"
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent(f"""
+        import os, sys
+        with open({str(log)!r}, "a") as f:
+            f.write(os.environ.get({RESUME_ENV!r}, "-") + "\\n")
+        with open(os.environ[{RUN_ID_ENV!r}], "w") as f:
+            f.write("exp-9\\n4")
+        sys.exit({EXIT_TIMEOUT})
+    """))
+    rc = supervise(lambda a: [sys.executable, str(child), *a], [], max_restarts=5)
+    assert rc == EXIT_TIMEOUT
+    assert log.read_text().split() == ["-", "1"]          # first run + one relaunch, then it gives up
+    f = tmp_path / "id"
+    import os
+    os.environ[RUN_ID_ENV] = str(f)
+    try:
+        record_run_id("abc", 7)
+    finally:
+        del os.environ[RUN_ID_ENV]
+    assert read_run_id(str(f)) == ("abc", 7)
+
+
+def test_watchdog_scales_with_shard_and_is_off_for_cpu_runs(monkeypatch):
+    from serann.utils.faults import JOB_ORGANISMS, GenerationWatchdog, job_scale
+    assert job_scale(0) == 1 and job_scale(JOB_ORGANISMS) == 1 and job_scale(JOB_ORGANISMS + 1) == 2
+    assert job_scale(10, waves=3) == 3
+    wd = GenerationWatchdog(10.0)
+    wd.arm("g", job_scale(300))
+    assert wd._armed_s == 30.0
+    wd.disarm()
+    from serann.cli.launch import CHILD_ENV
+    from serann.experiment.experiment import Experiment
+    monkeypatch.delenv(CHILD_ENV, raising=False)
+
+    class W:
+        engine_name = "torch"
+    e = Experiment("x", None, W(), None, {"genotype_size": 8, "num_classification_classes": 10}, None)
+    assert e._watchdog.timeout_s == 0           # CPU engine, unsupervised: never armed
+    W.engine_name = "hip"
+    e = Experiment("x", None, W(), None, {"genotype_size": 8, "num_classification_classes": 10}, None)
+    assert e._watchdog.timeout_s > 0
 
 
 def test_collective_timeout_follows_job_timeout(monkeypatch):

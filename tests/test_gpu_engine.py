@@ -233,6 +233,43 @@ def test_fit_graph_replay_learns():
     assert np.array_equal(np.unpackbits(pb.cpu().numpy(), axis=-1)[..., :100], np.stack([replication_bits(o) for o in ob]))
 
 
+def test_engines_in_sequence_in_one_process():
+    """Several engines built, fitted (captured graph), evaluated, replicated and closed one after another
+    in one process -- the driver runs the whole GPU suite as one pytest process -- plus a second fit on one
+    engine (its cached inference plan must stay valid), the mutant with host fallbacks included.  Device
+    memory returns to its starting level once the engines and datasets are gone."""
+    import gc
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import _DEVICE_DATA, HipPopulationEngine
+    torch.cuda.synchronize()
+    gc.collect()
+    base = torch.cuda.memory_allocated()
+    cfg = TrainConfig(epochs=1, batch_size=250)
+    pops = [("conv_pool_dense", "mutant_neg_sub"), ("odd_channels_bn", "gchain_f64_bn_dense", "rewired_fanout"),
+            ("narrow_bn_ancestor", "convpool_bench_a")]
+    for k, names in enumerate(pops):
+        data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=2000, n_test=500, seed=10 + k),
+                               n_train=2000, n_test=500)
+        irs = [interpret(ARCHS[n]) for n in names]
+        eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
+        for rep in range(2 if k == 0 else 1):
+            res = eng.fit(data, cfg)
+            assert eng.graph is not None and np.all(np.isfinite(res.val_acc)), (names, rep)
+            acc = eng.evaluate(data.test_x, data.test_labels, data.test_g, cfg)
+            assert np.all(np.isfinite(acc))
+        gen = np.random.default_rng(k).integers(0, 2, (len(irs), 100)).astype(np.float32)
+        packed = eng.replicate_packed(gen, [data.test_x[:40]] * len(irs), cfg)
+        assert packed.shape == (len(irs), 40, 13)
+        eng.close()
+        assert eng.graph is None and not eng.plans
+        del eng, packed, data
+        gc.collect()
+        torch.cuda.synchronize()
+    assert len(_DEVICE_DATA) == 0                    # uploads died with their datasets
+    assert torch.cuda.memory_allocated() - base < 64 << 20, torch.cuda.memory_allocated() - base
+
+
 def test_fit_remainder_batch_matches_torch():
     """A batch size that does not divide the training split: the last step of each epoch trains on
     the true remainder (Keras semantics), in the HIP engine as in the torch oracle.  BatchNorm moving
@@ -466,20 +503,3 @@ def test_adam_kernel_matches_keras_formula():
     assert torch.all(g == 0)
     assert int(step.item()) == 1
     assert torch.allclose(pbf.float(), ref, atol=1e-2, rtol=1e-2)
-
-
-def test_popstats_kernel():
-    from serann.ops import hip_ops as H
-    from scipy.spatial.distance import pdist
-    rng = np.random.default_rng(0)
-    gen = rng.integers(0, 2, (300, 100)).astype(np.uint8)
-    bits = np.packbits(gen, axis=-1)
-    bits = np.pad(bits, ((0, 0), (0, 16 - bits.shape[1]))).view(np.uint64)
-    tb = torch.as_tensor(bits.view(np.int64), device="cuda")
-    out = torch.zeros(2, dtype=torch.float64, device="cuda")
-    H.lib().popstats(tb.data_ptr(), 300, 2, out.data_ptr(), H.stream_handle())
-    torch.cuda.synchronize()
-    sh, se = out.cpu().numpy()
-    npairs = 300 * 299 / 2
-    assert abs(sh / npairs / 100 - pdist(gen, "hamming").mean()) < 1e-9
-    assert abs(se / npairs - pdist(gen).mean()) < 1e-9

@@ -110,16 +110,16 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape):
     B, Hh, Ww, C, Fo, KH, KW, SH, SW, act = shape
     OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
     g = torch.Generator(device=DEV).manual_seed(0)
-    x = torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16()
-    w = (torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16()   # Wm layout
-    bias = torch.randn(Fo, device=DEV, generator=g)
-    dz = torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16()
+    x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16())
+    w = H.padded((torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16())  # Wm layout
+    bias = H.padded(torch.randn(Fo, device=DEV, generator=g))
+    dz = H.padded(torch.randn(B, OH, OW, Fo, device=DEV, generator=g).bfloat16())
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)            # (F, C, KH, KW)
     ref = ref_conv2d(xr, wr, bias, (SH, SW)).permute(0, 2, 3, 1)
     ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](ref)
     # FWD
-    y = torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV)
+    y = H.padded(torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV))
     K = KH * KW * C
     flags = (H.GF_VEC_A if C % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
@@ -128,10 +128,10 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape):
               [(B * OH * OW, Fo, K)])
     assert _rel(y.float(), ref) < 6e-3
     # DGRAD
-    dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
+    dx = H.padded(torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV))
     ref_dx = ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     flags = (H.GF_VEC_A if Fo % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
-    wt = w.permute(3, 1, 2, 0).contiguous()       # Wt[C][KH][KW][F] for the register-fragment DGRAD kernel
+    wt = H.padded(w.permute(3, 1, 2, 0).contiguous())  # Wt[C][KH][KW][F] for the register-fragment DGRAD kernel
     _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), _bnat=w.data_ptr(), out=dx.data_ptr(),
                                   M=B * Hh * Ww, N=C, K=KH * KW * Fo, flags=flags, **geo)],
               [(B * Hh * Ww, C, KH * KW * Fo)])
@@ -140,7 +140,7 @@ def test_grouped_conv_fwd_dgrad_wgrad(shape):
     ref_dw = ref_conv2d_weight(xr, wr.shape, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     res = []
     for _ in range(2):
-        dw = torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV)
+        dw = H.padded(torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV))
         _run_gemm(H.MODE_WGRAD, [dict(a=dz.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), M=Fo, N=K, K=B * OH * OW,
                                       flags=flags, **geo)], [(Fo, K, B * OH * OW)])
         res.append(dw)
@@ -157,10 +157,10 @@ def test_tiled_fwd_split_k_with_finalize():
              (750, 135, 6944, "relu"), (750, 190, 2100, "sigmoid"), (500, 250, 3000, "linear")]
     rows, dims, refs, outs, keep = [], [], [], [], []
     for M, N, K, act in probs:
-        x = torch.randn(M, K, device=DEV).bfloat16()
-        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-        b = torch.randn(N, device=DEV)
-        y = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        x = H.padded(torch.randn(M, K, device=DEV).bfloat16())
+        w = H.padded((torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16())
+        b = H.padded(torch.randn(N, device=DEV))
+        y = H.padded(torch.zeros(M, N, dtype=torch.bfloat16, device=DEV))
         keep += [x, w, b, y]
         rows.append(dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), H=1, W=1, C=K, OH=1, OW=1,
                          F=N, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=K, act=H.ACT_CODES[act],
@@ -177,7 +177,7 @@ def test_tiled_fwd_split_k_with_finalize():
             ns = int(r.pop("_split", 1))
             if ns > 1:
                 nsplit += 1
-                wsb = torch.full((ns * r["M"] * r["N"],), float("nan"), device=DEV)   # every slot is written
+                wsb = H.padded(torch.full((ns * r["M"] * r["N"],), float("nan"), device=DEV))  # every slot is written
                 keep.append(wsb)
                 r["aux"] = wsb.data_ptr()
                 fin.append(dict(ws=r["aux"], out=r["out"], bias=r["bias"], M=r["M"], N=r["N"], S=ns, act=r["act"]))
@@ -203,14 +203,14 @@ def test_tiled_dgrad_natural_weights(M, N, F, D, col, act):
     transposed copy), optionally a column slice [col, col + N) of a wider weight matrix (fused concat),
     with dZ = dY * act'(Y) fused on load."""
     torch.cuda.synchronize()
-    dy = torch.randn(M, F, device=DEV).bfloat16()
-    y = torch.randn(M, F, device=DEV).bfloat16()
+    dy = H.padded(torch.randn(M, F, device=DEV).bfloat16())
+    y = H.padded(torch.randn(M, F, device=DEV).bfloat16())
     if act == "relu":
-        y = torch.relu(y)
+        y = H.padded(torch.relu(y))
     elif act == "sigmoid":
-        y = torch.sigmoid(y.float()).bfloat16()
-    w = (torch.randn(F, D, device=DEV) / math.sqrt(F)).bfloat16()
-    dx = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        y = H.padded(torch.sigmoid(y.float()).bfloat16())
+    w = H.padded((torch.randn(F, D, device=DEV) / math.sqrt(F)).bfloat16())
+    dx = H.padded(torch.zeros(M, N, dtype=torch.bfloat16, device=DEV))
     row = dict(a=dy.data_ptr(), b=0, _bnat=w.data_ptr() + 2 * col, _bnat_ld=D, aux=y.data_ptr(), act=H.ACT_CODES[act],
                out=dx.data_ptr(), H=1, W=1, C=N, OH=1, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=N, K=F, flags=0)
     plans = H.gemm3_plan(H.MODE_DGRAD, [row], [(M, N, F)])
@@ -227,8 +227,8 @@ def test_tiled_dgrad_natural_weights(M, N, F, D, col, act):
 
 
 def test_transpose_weights_kernel():
-    w = torch.randn(37, 3, 5, 13, device=DEV).bfloat16()
-    out = torch.zeros(13, 3, 5, 37, dtype=torch.bfloat16, device=DEV)
+    w = H.padded(torch.randn(37, 3, 5, 13, device=DEV).bfloat16())
+    out = H.padded(torch.zeros(13, 3, 5, 37, dtype=torch.bfloat16, device=DEV))
     d = _desc([dict(src=w.data_ptr(), dst=out.data_ptr(), F=37, P=15, C=13)], H.TRANS_DTYPE)
     t = torch.as_tensor(H.chunk_tiles([-(-w.numel() // H.TRANS_ELEMS)], 1), device=DEV)
     H.lib().transpose_weights(d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
@@ -241,9 +241,9 @@ def test_grouped_gemm_many_problems_one_launch():
     keep = []
     for i, (B, Hh, Ww, C, Fo, KH, KW, SH, SW, act) in enumerate(SHAPES):
         OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
-        x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
-        w = (torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16()
-        y = torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV)
+        x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
+        w = H.padded((torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16())
+        y = H.padded(torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV))
         keep += [x, w, y]
         K = KH * KW * C
         rows.append(dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH,
@@ -261,16 +261,16 @@ def test_grouped_gemm_many_problems_one_launch():
                                 (24576, 1), (96000, 128), (363000, 16)])
 def test_bn_train_infer_backward(RC):
     R, C = RC
-    x = (torch.randn(R, C, device=DEV) * 3 + 1).bfloat16()
-    gamma = torch.rand(C, device=DEV) + 0.5
-    beta = torch.randn(C, device=DEV)
-    mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
-    mean, invstd = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-    ws = torch.zeros(H.bn_ws_words(C), dtype=torch.int64, device=DEV)
-    y = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
-    dy = torch.randn(R, C, device=DEV).bfloat16()
-    dx = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
-    dg, db = (torch.zeros(C, dtype=torch.int64, device=DEV) for _ in range(2))     # Q32 gradient arena
+    x = H.padded((torch.randn(R, C, device=DEV) * 3 + 1).bfloat16())
+    gamma = H.padded(torch.rand(C, device=DEV) + 0.5)
+    beta = H.padded(torch.randn(C, device=DEV))
+    mm, mv = H.padded(torch.zeros(C, device=DEV)), H.padded(torch.ones(C, device=DEV))
+    mean, invstd = H.padded(torch.zeros(C, device=DEV)), H.padded(torch.zeros(C, device=DEV))
+    ws = H.padded(torch.zeros(H.bn_ws_words(C), dtype=torch.int64, device=DEV))
+    y = H.padded(torch.zeros(R, C, dtype=torch.bfloat16, device=DEV))
+    dy = H.padded(torch.randn(R, C, device=DEV).bfloat16())
+    dx = H.padded(torch.zeros(R, C, dtype=torch.bfloat16, device=DEV))
+    dg, db = (H.operand(C, torch.int64, DEV) for _ in range(2))     # Q32 gradient arena
     row = dict(x=x.data_ptr(), y=y.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), gamma=gamma.data_ptr(),
                beta=beta.data_ptr(), mm=mm.data_ptr(), mv=mv.data_ptr(), mean=mean.data_ptr(), invstd=invstd.data_ptr(),
                ws=ws.data_ptr(), dgamma=dg.data_ptr(), dbeta=db.data_ptr(), R=R, C=C, flags=3, eps=1e-3, momentum=0.99)
@@ -280,7 +280,7 @@ def test_bn_train_infer_backward(RC):
     L, s = H.lib(), H.stream_handle()
     L.bn(0, d.data_ptr(), ts.data_ptr(), len(ts), s)
     torch.cuda.synchronize()
-    ws0 = ws.clone()
+    ws0 = H.padded(ws.clone())
     ws.zero_()
     L.bn(0, d.data_ptr(), ts.data_ptr(), len(ts), s)        # statistics again: bitwise identical
     torch.cuda.synchronize()
@@ -318,10 +318,10 @@ def test_maxpool_fwd_bwd(p, C):
     PH, PW, SH, SW = p
     B, Hh, Ww = 3, 13, 11
     OH, OW = (Hh - PH) // SH + 1, (Ww - PW) // SW + 1
-    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
-    y = torch.zeros(B, OH, OW, C, dtype=torch.bfloat16, device=DEV)
-    idx = torch.zeros(B * OH * OW * C, dtype=torch.uint8, device=DEV)
-    dy = torch.randn(B, OH, OW, C, device=DEV).bfloat16()
+    x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
+    y = H.padded(torch.zeros(B, OH, OW, C, dtype=torch.bfloat16, device=DEV))
+    idx = H.padded(torch.zeros(B * OH * OW * C, dtype=torch.uint8, device=DEV))
+    dy = H.padded(torch.randn(B, OH, OW, C, device=DEV).bfloat16())
     dx = torch.zeros_like(x)
     row = dict(x=x.data_ptr(), y=y.data_ptr(), idx=idx.data_ptr(), dy=dy.data_ptr(), dx=dx.data_ptr(), B=B, H=Hh, W=Ww,
                C=C, OH=OH, OW=OW, PH=PH, PW=PW, SH=SH, SW=SW, flags=0)
@@ -341,11 +341,11 @@ def test_maxpool_fwd_bwd(p, C):
 
 def test_loss_kernel_matches_keras_losses():
     B, NC, L_ = 50, 10, 100
-    z = torch.randn(B, NC + L_, device=DEV)
-    labels = torch.randint(0, NC, (B,), device=DEV, dtype=torch.int32)
-    tgt = torch.randint(0, 2, (B, L_), device=DEV).bfloat16()
-    dz = torch.zeros(B, NC + L_, dtype=torch.bfloat16, device=DEV)
-    metrics = torch.zeros(4, dtype=torch.int64, device=DEV)          # Q32 fixed point
+    z = H.padded(torch.randn(B, NC + L_, device=DEV))
+    labels = H.padded(torch.randint(0, NC, (B,), device=DEV, dtype=torch.int32))
+    tgt = H.padded(torch.randint(0, 2, (B, L_), device=DEV).bfloat16())
+    dz = H.padded(torch.zeros(B, NC + L_, dtype=torch.bfloat16, device=DEV))
+    metrics = H.padded(torch.zeros(4, dtype=torch.int64, device=DEV))  # Q32 fixed point
     lb = 0.3
     row = dict(logits=z.data_ptr(), dlogits=dz.data_ptr(), labels=labels.data_ptr(), target=tgt.data_ptr(),
                metrics=metrics.data_ptr(), NC=NC, L=L_, B=B, lb=lb)
@@ -372,18 +372,18 @@ def test_fused_act_grad_and_bias_grad(act, shape):
     B, Hh, Ww, C, Fo, KH, KW = shape
     SH = SW = 1
     OH, OW = Hh - KH + 1, Ww - KW + 1
-    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
-    w = (torch.randn(Fo, KH, KW, C, device=DEV) / 6).bfloat16()
-    ypre = torch.randn(B, OH, OW, Fo, device=DEV)
-    y = (torch.relu(ypre) if act == "relu" else torch.sigmoid(ypre)).bfloat16()
-    dy = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
+    x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
+    w = H.padded((torch.randn(Fo, KH, KW, C, device=DEV) / 6).bfloat16())
+    ypre = H.padded(torch.randn(B, OH, OW, Fo, device=DEV))
+    y = H.padded((torch.relu(ypre) if act == "relu" else torch.sigmoid(ypre)).bfloat16())
+    dy = H.padded(torch.randn(B, OH, OW, Fo, device=DEV).bfloat16())
     yf = y.float()
     dz = dy.float() * ((yf > 0).float() if act == "relu" else yf * (1 - yf))
     dz = dz.bfloat16().float()
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
     K = KH * KW * C
-    dw = torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV)
-    db = torch.zeros(Fo, dtype=torch.int64, device=DEV)
+    dw = H.padded(torch.zeros(Fo, KH, KW, C, dtype=torch.int64, device=DEV))
+    db = H.padded(torch.zeros(Fo, dtype=torch.int64, device=DEV))
     _run_gemm(H.MODE_WGRAD, [dict(a=dy.data_ptr(), b=x.data_ptr(), out=dw.data_ptr(), bias=db.data_ptr(),
                                   aux=y.data_ptr(), act=H.ACT_CODES[act], M=Fo, N=K, K=B * OH * OW, **geo)],
               [(Fo, K, B * OH * OW)])
@@ -393,8 +393,8 @@ def test_fused_act_grad_and_bias_grad(act, shape):
     ref_dw = ref_conv2d_weight(xr, wr.shape, dz.permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dw, ref_dw) < 1e-3
     assert _rel(db, dz.sum((0, 1, 2))) < 1e-3
-    dx = torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV)
-    wt = w.permute(3, 1, 2, 0).contiguous()
+    dx = H.padded(torch.zeros(B, Hh, Ww, C, dtype=torch.bfloat16, device=DEV))
+    wt = H.padded(w.permute(3, 1, 2, 0).contiguous())
     _run_gemm(H.MODE_DGRAD, [dict(a=dy.data_ptr(), b=wt.data_ptr(), _bnat=w.data_ptr(), out=dx.data_ptr(),
                                   aux=y.data_ptr(), act=H.ACT_CODES[act], M=B * Hh * Ww, N=C, K=KH * KW * Fo, **geo)],
               [(B * Hh * Ww, C, KH * KW * Fo)])
@@ -405,10 +405,10 @@ def test_fused_act_grad_and_bias_grad(act, shape):
 def test_wave_split_k_dense():
     """Few rows, long K (the Dense-on-merge shape): the wave-split-K form must match."""
     M, K, N = 750, 5003, 110
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    w = (torch.randn(N, K, device=DEV) / 70).bfloat16()
-    b = torch.randn(N, device=DEV)
-    y = torch.zeros(M, N, device=DEV)
+    x = H.padded(torch.randn(M, K, device=DEV).bfloat16())
+    w = H.padded((torch.randn(N, K, device=DEV) / 70).bfloat16())
+    b = H.padded(torch.randn(N, device=DEV))
+    y = H.padded(torch.zeros(M, N, device=DEV))
     geo = dict(H=1, W=1, C=K, OH=1, OW=1, F=N, KH=1, KW=1, SH=1, SW=1)
     assert 100 <= H.gemm3_variant(H.MODE_FWD, M, N, K, geo) % 1000
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), bias=b.data_ptr(), M=M, N=N, K=K,
@@ -424,20 +424,20 @@ def test_v3_accumulating_outputs(shape):
     through both the coalesced LDS-staged epilogue and the scattered one."""
     B, Hh, Ww, C, Fo, KH, KW, SH, SW = shape
     OH, OW = (Hh - KH) // SH + 1, (Ww - KW) // SW + 1
-    x = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
-    w = (torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16()
-    dz = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
+    x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
+    w = H.padded((torch.randn(Fo, KH, KW, C, device=DEV) / math.sqrt(KH * KW * C)).bfloat16())
+    dz = H.padded(torch.randn(B, OH, OW, Fo, device=DEV).bfloat16())
     xr, wr = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)
     geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=SH, SW=SW)
-    prev = torch.randn(B, Hh, Ww, C, device=DEV).bfloat16()
-    dx = prev.clone()
-    wt = w.permute(3, 1, 2, 0).contiguous()
+    prev = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
+    dx = H.padded(prev.clone())
+    wt = H.padded(w.permute(3, 1, 2, 0).contiguous())
     _run_gemm(H.MODE_DGRAD, [dict(a=dz.data_ptr(), b=wt.data_ptr(), out=dx.data_ptr(), M=B * Hh * Ww, N=C,
                                   K=KH * KW * Fo, flags=H.GF_ACCUM, **geo)], [(B * Hh * Ww, C, KH * KW * Fo)])
     ref = prev.float() + ref_conv2d_input(xr.shape, wr, dz.float().permute(0, 3, 1, 2), (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(dx.float(), ref) < 6e-3
-    prev_y = torch.randn(B, OH, OW, Fo, device=DEV).bfloat16()
-    y = prev_y.clone()
+    prev_y = H.padded(torch.randn(B, OH, OW, Fo, device=DEV).bfloat16())
+    y = H.padded(prev_y.clone())
     _run_gemm(H.MODE_FWD, [dict(a=x.data_ptr(), b=w.data_ptr(), out=y.data_ptr(), M=B * OH * OW, N=Fo,
                                 K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)])
     ref_y = prev_y.float() + ref_conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)

@@ -291,3 +291,18 @@ def test_riboae_loss_uses_hip_path_and_matches(monkeypatch):
     gmax = max(float(g.abs().max()) for g in gb)
     for x1, x2 in zip(ga, gb):
         assert torch.allclose(x1, x2, rtol=1e-2, atol=1e-4 * gmax)
+
+
+def test_arena_only_optimizer_state_restarts_adam_cpu():
+    """An arena-only (old HIP) optimizer state on the torch engine: Adam restarts at t = 0 with zero
+    moments instead of keeping a large t over fresh moments (trainer.py)."""
+    from serann.riboae.trainer import ScheduledKerasAdam
+    p = [torch.nn.Parameter(torch.ones(3)), torch.nn.Parameter(torch.ones(2, 2))]
+    opt = ScheduledKerasAdam(p, lr=1e-3, eps=1e-7)
+    opt.m[0].fill_(5.0)
+    opt.t = 7
+    opt.load_state_dict({"t": 900, "m_arena": torch.zeros(8), "v_arena": torch.zeros(8)})
+    assert opt.t == 0 and float(opt.m[0].abs().sum()) == 0.0
+    opt.load_state_dict({"t": 4, "m": [torch.full((3,), 2.0), torch.full((2, 2), 3.0)],
+                         "v": [torch.ones(3), torch.ones(2, 2)]})
+    assert opt.t == 4 and float(opt.m[1][0, 0]) == 3.0

@@ -116,3 +116,30 @@ def test_hip_loss_curve_matches_torch_path(tmp_path):
     assert abs(a - b) < 0.02 * abs(b), (a, b)
     m2, ck = load_checkpoint(str(tmp_path / "r_hip_b200.pt"))
     assert ck["step"] == 200 and "m_arena" in ck["optimizer"]
+
+
+def test_checkpoint_moments_cross_engines(tmp_path):
+    """A HIP checkpoint resumes on the torch engine and a torch checkpoint on the HIP engine with the
+    same Adam moments and step count (the formats used not to convert)."""
+    from serann.riboae.hip_trainer import HipRiboTrainer
+    from serann.riboae.trainer import ScheduledKerasAdam
+    x, u = _batch(32, seed=5)
+    m = _model(6).cuda().train()
+    tr = HipRiboTrainer(m, device="cuda")
+    for _ in range(3):
+        tr.step(x.cuda(), 0.3, 0.05, 3e-4, noise=u.cuda())
+    st = tr.state_dict()
+    assert st["t"] == 3 and len(st["m"]) == len(list(m.parameters()))
+    # HIP -> torch: the per-parameter lists are the arena moments in torch layout
+    opt = ScheduledKerasAdam(list(m.parameters()), lr=3e-4, eps=1e-7)
+    opt.load_state_dict(st)
+    assert opt.t == 3
+    for a, b in zip(opt.m, tr._moment_views(tr.m)):
+        assert torch.equal(a.cpu(), b.cpu())
+    # torch -> HIP: a fresh trainer restores the moments from the lists alone
+    m2 = _model(6).cuda().train()
+    tr2 = HipRiboTrainer(m2, device="cuda")
+    tr2.load_state_dict({"t": opt.t, "m": opt.state_dict()["m"], "v": opt.state_dict()["v"]})
+    n = tr.pa.size
+    assert int(tr2.step_i.item()) == 3
+    assert torch.equal(tr2.m[:n].cpu(), tr.m[:n].cpu()) and torch.equal(tr2.v[:n].cpu(), tr.v[:n].cpu())
