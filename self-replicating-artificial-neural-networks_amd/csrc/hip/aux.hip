@@ -978,9 +978,9 @@ __global__ __launch_bounds__(256) void rep_bits_kernel(const RepBitsDesc* __rest
     reinterpret_cast<uint8_t*>(d.out)[e] = (uint8_t)byte;
 }
 
-void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream) {
-    if (ndesc <= 0 || max_rows <= 0) return;
-    const int64_t bytes = max_rows * 32;                 // >= rows * ceil(L / 8) for L <= 256
+void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, int64_t row_bytes, uint64_t stream) {
+    if (ndesc <= 0 || max_rows <= 0 || row_bytes <= 0) return;
+    const int64_t bytes = max_rows * row_bytes;          // row_bytes = max over problems of ceil(L / 8)
     hipLaunchKernelGGL(rep_bits_kernel, dim3((unsigned)((bytes + 255) / 256), (unsigned)ndesc), dim3(256), 0,
                        as_stream(stream), as_ptr<const RepBitsDesc>(descs));
     SERANN_CHECK(hipGetLastError());

@@ -59,6 +59,11 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act) {
 //    2^-32 = 2.3e-10 absolute (below the bf16 operand noise of any gradient that can move an Adam
 //    update with eps = 1e-4), final sums within +-2^31.  Each contribution is clamped to +-2^30 first
 //    (NaN -> -2^30) so the conversion is always defined.
+//    The RiboAE trainer (riboae/hip_trainer.py) reuses this arena with Keras' eps = 1e-7, where the
+//    argument above is weaker: a gradient element below 2^-33 (1.2e-10) flushes to zero and one near
+//    1e-9 carries ~10 % quantisation error, while Adam scales g / (|g| + 1e-7) to ~1 % of lr there.
+//    Such elements move a parameter by <= 1e-2 lr per step either way (they are the dead tail of the
+//    embedding / Dense gradients); the RiboAE gradient test bounds every parameter's error against fp32.
 //  * fxw ("wide", two words hi, lo): BatchNorm statistics (sums of squares over up to 588k rows).  A
 //    contribution q = round(v * 2^32) is split as hi = q >> 32, lo = q & (2^32 - 1) (lo >= 0); the
 //    words are summed separately, total = hi + lo * 2^-32: same resolution, range +-2^63.

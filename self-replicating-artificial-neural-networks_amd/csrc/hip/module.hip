@@ -13,6 +13,7 @@ static py::dict desc_sizes() {
     d["BnDesc"] = sizeof(BnDesc);
     d["PoolDesc"] = sizeof(PoolDesc);
     d["CopyDesc"] = sizeof(CopyDesc);
+    d["EwDesc"] = sizeof(EwDesc);
     d["LossDesc"] = sizeof(LossDesc);
     d["TransDesc"] = sizeof(TransDesc);
     d["ImcolDesc"] = sizeof(ImcolDesc);
@@ -43,6 +44,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("convpool", &launch_convpool);
     m.def("gchain", &launch_gchain);
     m.def("copy2d", &launch_copy2d);
+    m.def("ew", &launch_ew);
     m.def("loss", &launch_loss);
     m.def("memset32", &launch_memset32);
     m.def("group_argmax", &launch_group_argmax);

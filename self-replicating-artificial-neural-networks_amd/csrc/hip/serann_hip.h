@@ -59,6 +59,7 @@ void launch_gather_batch(uint64_t x_all, uint64_t g_all, uint64_t y_all, uint64_
 void launch_counter_add(uint64_t counter, int64_t value, uint64_t stream);
 void launch_bn(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_pool(int backward, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+void launch_ew(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_copy2d(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t stream, int64_t nvalid);
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
@@ -96,6 +97,15 @@ struct BnDesc {
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum
 struct CopyDesc { int64_t src, dst, rows, cols, src_stride, dst_stride, flags; };           // flags: 1 accum
+// Strided elementwise map / reduction (ew.hip): out[j] (+)= sum_r (ca A[a(j,r)] + cb B[b(j,r)]) + c over a
+// dense 4-d destination D and a 4-d reduction box R; strides in elements; b = 0: no B; flags: 1 accumulate
+struct EwDesc {
+    int64_t a, b, out;
+    int64_t D[4], R[4], aJ[4], aR[4], bJ[4], bR[4];
+    float ca, cb, c, pad;
+    int64_t flags;
+};
+constexpr int EW_ELEMS = 2048;        // destination elements per block
 struct SplitFinDesc { int64_t ws, out, bias, M, N, S, act, flags; };      // flags: 1 = fp32 output
 // Fused first-layer Conv2D + MaxPool2D on a raw single-channel image (convpool.hip).  w: bf16 [F][KH*KW];
 // bias / dw / dbias: fp32 (0 = none); y / dy: bf16 pooled [B][POH][POW][F]; idx: u8 argmax window offset.
@@ -139,7 +149,7 @@ void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float
 void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
                         float b1, float b2, float eps, uint64_t skip, uint64_t stream);
 void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
-void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, uint64_t stream);
+void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, int64_t row_bytes, uint64_t stream);
 struct LossDesc {
     int64_t logits, dlogits, labels, target, metrics, NC, L, B, flags;
     double lb;

@@ -15,8 +15,10 @@ Weights use the output-major layout ``Wm[F][KH][KW][C]`` (the forward GEMM's B o
 k-contiguous); the two heads of an organism are stored adjacently as one ``[NC+L][D]`` matrix so
 they run as a single GEMM with an fp32 output.
 
-Rare ops reachable only by mutation (unary/binary minus, BatchNormalization on a non-last axis)
-run through a torch fallback inside the same plan (still graph-captured).
+Rare ops reachable only by mutation (unary / binary minus with broadcasting, BatchNormalization on a
+non-last axis) run on the strided elementwise kernel (csrc/hip/ew.hip): maps, broadcast-gradient
+reductions and the [outer][C][inner] <-> [outer][inner][C] transposes around the channels-last BN
+kernels -- no host-driven torch op anywhere in a plan.
 """
 from __future__ import annotations
 
@@ -262,7 +264,6 @@ class Launch:
     descs: Optional[torch.Tensor]
     tiles: Optional[torch.Tensor]
     n: int
-    fn: object = None
 
 
 class Plan:
@@ -295,10 +296,10 @@ class Plan:
                 L.nbn(la.arg[0], la.arg[1], la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "copy":
                 L.copy2d(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "ew":
+                L.ew(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "splitfin":
                 L.splitk_finalize(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
-            elif k == "fn":
-                la.fn()
             else:
                 raise ValueError(k)
 
@@ -318,9 +319,6 @@ class HipPopulationEngine(PopulationEngine):
         self.plans: Dict[tuple, Plan] = {}
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.timings: Dict[str, float] = {}
-        # raw input buffers by device address (the torch fallbacks of rare ops view them); entries are only
-        # ever added -- every plan keeps its buffers alive, so an address cannot be reused while listed
-        self._input_tensors: Dict[int, torch.Tensor] = {}
 
     # ---------------------------------------------------------------------------------------------
     # parameters
@@ -512,6 +510,11 @@ class HipPopulationEngine(PopulationEngine):
                 if n.op == "bn":
                     c = n.attrs["channels"]
                     rec["bn"][n.id] = {"mean": f32.alloc(c), "invstd": f32.alloc(c), "ws": None, "wsb": None}
+                    if not n.attrs["last"]:
+                        # a BatchNormalization on a non-last axis runs channels-last on transposed copies
+                        # (ew.hip permutes): input / output [outer][inner][C], their gradients likewise
+                        size = B * math.prod(n.shape)
+                        rec["bn"][n.id].update(xt=act.alloc(size), yt=act.alloc(size))
             if with_grads:
                 req = self._requires_grad(ir)
                 for n in ir.nodes:
@@ -524,6 +527,9 @@ class HipPopulationEngine(PopulationEngine):
                         rec["grad"][n.id] = grad.alloc(B * (NC + L))
                     elif req[n.id]:
                         rec["grad"][n.id] = grad.alloc(B * math.prod(n.shape))
+                    if n.op == "bn" and not n.attrs["last"] and req[n.id]:
+                        size = B * math.prod(n.shape)
+                        rec["bn"][n.id].update(dyt=grad.alloc(size), dxt=grad.alloc(size))
                 rec["req"] = req
             bufs.append(rec)
         # BN statistics workspaces (wide fixed point: [stripe][2C][hi, lo] int64, csrc/hip/common.h fxw_*),
@@ -921,7 +927,7 @@ class HipPopulationEngine(PopulationEngine):
             c_rows, c_cnt = [], []
             cp_rows = []
             gc_rows = []
-            fallbacks = []
+            ew_pre, ew_post = [], []          # rare ops (ew.hip): maps / transposes in, transposes out
             for o, lay in org_iter():
                 ir = lay.ir
                 rec = mem["orgs"][o]
@@ -1038,8 +1044,47 @@ class HipPopulationEngine(PopulationEngine):
                                                rows=outer, cols=inner, src_stride=inner, dst_stride=out_inner))
                             c_cnt.append(-(-outer // H.COPY_ROWS))
                             col += inner
+                    elif n.op == "bn":
+                        # non-last axis: [outer][C][inner] -> [outer][inner][C], the channels-last BN kernels,
+                        # and back (SURVEY §2.7 mutants; the reference runs it inside its Keras graph)
+                        bd = rec["bn"][n.id]
+                        c = a["channels"]
+                        full = (B,) + tuple(n.shape)
+                        outer, inner = math.prod(full[:a["axis"]]), math.prod(full[a["axis"] + 1:])
+                        xt, yt = mem["act"].ptr(bd["xt"]), mem["act"].ptr(bd["yt"])
+                        ew_pre.append(H.ew_permute_row(xt, self._act_ptr(mem, o, n.inputs[0], inputs),
+                                                       (outer, c, inner), (0, 2, 1)))
+                        ew_post.append(H.ew_permute_row(self._act_ptr(mem, o, n.id, inputs), yt, (outer, inner, c),
+                                                        (0, 2, 1)))
+                        flags = (1 if n.id in lay.gamma else 0) | (2 if n.id in lay.beta else 0)
+                        bn_rows.append(dict(x=xt, y=yt,
+                                            gamma=pptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                            beta=pptr(lay.beta[n.id]) if n.id in lay.beta else 0,
+                                            mm=sptr(lay.mm[n.id]), mv=sptr(lay.mv[n.id]),
+                                            mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
+                                            ws=mem["ws"].ptr(bd["ws"]), R=outer * inner, C=c,
+                                            flags=flags, eps=a["epsilon"], momentum=a["momentum"]))
+                        bn_cnt.append(H.bn_chunks(outer * inner, c))
+                        bn_cnt_st.append(H.bn_chunks(outer * inner, c, stats=True))
+                        bn_stat.append(True)
+                    elif n.op in ("neg", "sub"):
+                        full = (B,) + tuple(n.shape)
+                        out = self._act_ptr(mem, o, n.id, inputs)
+                        x0 = self._act_ptr(mem, o, n.inputs[0], inputs)
+                        s0 = (B,) + tuple(ir.node(n.inputs[0]).shape)
+                        if n.op == "neg":
+                            ew_pre.append(H.ew_map_row(out, full, x0, s0, ca=-1.0))
+                        elif a["mode"] == "tt":
+                            ew_pre.append(H.ew_map_row(out, full, x0, s0, ca=1.0,
+                                                       b=self._act_ptr(mem, o, n.inputs[1], inputs),
+                                                       b_shape=(B,) + tuple(ir.node(n.inputs[1]).shape), cb=-1.0))
+                        elif a["mode"] == "tc":
+                            ew_pre.append(H.ew_map_row(out, full, x0, s0, ca=1.0, c=-a["c"]))
+                        else:
+                            ew_pre.append(H.ew_map_row(out, full, x0, s0, ca=-1.0, c=a["c"]))
                     else:
-                        fallbacks.append((o, n))
+                        raise ValueError(f"organism {o}: no kernel for op {n.op!r}")
+            add_chunked("ew", 0, ew_pre, H.EW_DTYPE, [H.ew_count(r) for r in ew_pre], 1)
             add_gemm(H.MODE_FWD, g_rows, g_dims, extra_fin=fin_rows)
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             add_convpool(cp_rows, False)
@@ -1055,8 +1100,7 @@ class HipPopulationEngine(PopulationEngine):
                 else:
                     add_chunked("bn", 3, bn_rows, H.BN_DTYPE, bn_cnt, 1)
             add_chunked("copy", 0, c_rows, H.COPY_DTYPE, c_cnt, 1)
-            for o, n in fallbacks:
-                plan.launches.append(Launch("fn", 0, None, None, 0, self._fallback_fwd(mem, o, n, inputs, B, train)))
+            add_chunked("ew", 0, ew_post, H.EW_DTYPE, [H.ew_count(r) for r in ew_post], 1)
 
         if imcol:
             rows_ = [v["desc"] for v in imcol.values()]
@@ -1147,7 +1191,7 @@ class HipPopulationEngine(PopulationEngine):
                             and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
                         dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
 
-        STAGES = ("dgrad", "pool", "bn", "copy")
+        STAGES = ("dgrad", "pool", "bn", "copy", "ew")
         for d in range(maxd, 0, -1):
             wg_rows, wg_dims = [], []
             bn_red, bn_red_cnt = [], []
@@ -1155,7 +1199,7 @@ class HipPopulationEngine(PopulationEngine):
             gcb_rows = []
             nbnb_rows = []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
-            fb = []
+            ew_bpre = []                        # non-last-axis BN: dy -> channels-last dyt
             for o, lay in org_iter():
                 ir = lay.ir
                 rec = mem["orgs"][o]
@@ -1294,11 +1338,58 @@ class HipPopulationEngine(PopulationEngine):
                                 tasks["copy"].append((o, own, lambda acc, r=base: dict(r, flags=1 if acc else 0),
                                                       -(-outer // H.COPY_ROWS)))
                             col += inner
+                    elif n.op == "bn":
+                        # non-last axis (see the forward): BN backward on the channels-last copies, dx
+                        # transposed back into the input's gradient
+                        bd = rec["bn"][n.id]
+                        c = a["channels"]
+                        full = (B,) + tuple(n.shape)
+                        outer, inner = math.prod(full[:a["axis"]]), math.prod(full[a["axis"] + 1:])
+                        R = outer * inner
+                        dyt, dxt = mem["grad"].ptr(bd["dyt"]), mem["grad"].ptr(bd["dxt"])
+                        ew_bpre.append(H.ew_permute_row(dyt, mem["grad"].ptr(rec["grad"][n.id]), (outer, c, inner),
+                                                        (0, 2, 1)))
+                        own = target(o, n.inputs[0])
+                        pflags = (1 if n.id in lay.gamma else 0) | (2 if n.id in lay.beta else 0)
+                        base = dict(x=mem["act"].ptr(bd["xt"]), dy=dyt, dx=dxt,
+                                    gamma=pptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                    mean=f32a.ptr(bd["mean"]), invstd=f32a.ptr(bd["invstd"]),
+                                    ws=mem["ws"].ptr(bd["wsb"]),
+                                    dgamma=gptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,
+                                    dbeta=gptr(lay.beta[n.id]) if n.id in lay.beta else 0,
+                                    R=R, C=c, eps=a["epsilon"], momentum=a["momentum"])
+                        bn_red.append(dict(base, flags=pflags))
+                        bn_red_cnt.append(H.bn_chunks(R, c, stats=True))
+                        # dxt is private to this BN: overwritten (no accumulate); no dx at all without a target
+                        tasks["bn"].append((o, None, lambda acc, r=base, f=pflags, t=own: dict(r, flags=f | (8 if t is None else 0)),
+                                            H.bn_chunks(R, c)))
+                        if own is not None:
+                            tasks["ew"].append((o, own, lambda acc, r=(mem["grad"].ptr(rec["grad"][own]), dxt, (outer, inner, c)):
+                                                H.ew_permute_row(r[0], r[1], r[2], (0, 2, 1), accum=acc),
+                                                -(-B * math.prod(n.shape) // H.EW_ELEMS)))
+                    elif n.op in ("neg", "sub"):
+                        dy = mem["grad"].ptr(rec["grad"][n.id])
+                        full = (B,) + tuple(n.shape)
+                        if n.op == "neg":
+                            scales = [-1.0]
+                        elif a["mode"] == "tt":
+                            scales = [1.0, -1.0]
+                        else:
+                            scales = [1.0 if a["mode"] == "tc" else -1.0]
+                        for i, sc in zip(n.inputs, scales):
+                            own = target(o, i)
+                            if own is None:
+                                continue
+                            oshape = (B,) + tuple(ir.node(i).shape)
+                            tasks["ew"].append((o, own, lambda acc, r=(mem["grad"].ptr(rec["grad"][own]), oshape, dy, full, sc):
+                                                H.ew_reduce_row(r[0], r[1], r[2], r[3], r[4], accum=acc),
+                                                -(-math.prod(oshape) // H.EW_ELEMS)))
                     else:
-                        fb.append((o, n))
+                        raise ValueError(f"organism {o}: no backward kernel for op {n.op!r}")
             add_convpool(cpw_rows, True)
             add_gchain([r for r in gcb_rows if r["_bn"]], H.GC_BSTAT)
             add_gchain(gcb_rows, H.GC_BFULL)
+            add_chunked("ew", 0, ew_bpre, H.EW_DTYPE, [H.ew_count(r) for r in ew_bpre], 1)
             if bn_red:
                 add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
             add_nbn(nbnb_rows, 4)
@@ -1327,6 +1418,8 @@ class HipPopulationEngine(PopulationEngine):
                         add_chunked("pool", 1, rows, H.POOL_DTYPE, cnts, H.POOL_ELEMS)
                     elif stage == "bn":
                         add_chunked("bn", 5, rows, H.BN_DTYPE, cnts, 1)
+                    elif stage == "ew":
+                        add_chunked("ew", 0, rows, H.EW_DTYPE, cnts, 1)
                     else:
                         add_chunked("copy", 0, rows, H.COPY_DTYPE, cnts, 1)
             # WGRAD after this depth's DGRAD: a WGRAD that applies Adam to its tile (GF_ADAM) rewrites the
@@ -1335,156 +1428,12 @@ class HipPopulationEngine(PopulationEngine):
                 for r in wg_rows:
                     r["adam"] = adam_ctx
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
-            for o, n in fb:
-                plan.launches.append(Launch("fn", 0, None, None, 0,
-                                            self._fallback_bwd(mem, o, n, inputs, B, target, written)))
         # descriptor / tile tables are uploaded from pageable host memory: fence them (and any
         # outstanding work on other streams) before a launch can read them.  Plans are built once per
         # generation, so this costs nothing on the training hot path.
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         return plan
-
-    # ---------------------------------------------------------------------------------------------
-    # torch fallback for rare ops (neg / sub / BN on a non-last axis)
-    # ---------------------------------------------------------------------------------------------
-    def _view(self, mem, o, nid, inputs, B, grad=False):
-        ir = self.layouts[o].ir
-        n = ir.node(nid)
-        numel = B * math.prod(n.shape)
-        if grad:
-            p = self._grad_ptr(mem, o, nid)
-            arena, base = mem["grad"], mem["grad"].t
-        else:
-            p = self._act_ptr(mem, o, nid, inputs)
-            arena, base = mem["act"], mem["act"].t
-        off = (p - base.data_ptr()) // 2
-        if 0 <= off < base.numel():
-            return base.narrow(0, off, numel).view((B,) + n.shape)
-        # raw input buffers live outside the arena
-        t = self._input_tensors[p]
-        return t.reshape(-1).narrow(0, 0, numel).view((B,) + n.shape)
-
-    def _fallback_compute(self, o, n, xs, training):
-        a = n.attrs
-        lay = self.layouts[o]
-        if n.op == "neg":
-            return -xs[0]
-        if n.op == "sub":
-            m = a["mode"]
-            return xs[0] - xs[1] if m == "tt" else (xs[0] - a["c"] if m == "tc" else a["c"] - xs[0])
-        if n.op == "bn":
-            ax = a["axis"]
-            x = xs[0]
-            red = [i for i in range(x.dim()) if i != ax]
-            shp = [1] * x.dim()
-            shp[ax] = a["channels"]
-            c = a["channels"]
-            gamma = self.p.narrow(0, lay.gamma[n.id], c) if n.id in lay.gamma else None
-            beta = self.p.narrow(0, lay.beta[n.id], c) if n.id in lay.beta else None
-            mm = self.stats.narrow(0, lay.mm[n.id], c)
-            mv = self.stats.narrow(0, lay.mv[n.id], c)
-            if training:
-                mean = x.mean(red)
-                var = x.var(red, unbiased=False)
-                y = (x - mean.view(shp)) / torch.sqrt(var.view(shp) + a["epsilon"])
-            else:
-                y = (x - mm.view(shp)) / torch.sqrt(mv.view(shp) + a["epsilon"])
-            if gamma is not None:
-                y = y * gamma.view(shp)
-            if beta is not None:
-                y = y + beta.view(shp)
-            return y, (mean, var) if training else None
-        raise ValueError(n.op)
-
-    def _fallback_fwd(self, mem, o, n, inputs, B, train):
-        def fn():
-            xs = [self._view(mem, o, i, inputs, B).float() for i in n.inputs]
-            out = self._fallback_compute(o, n, xs, train)
-            if n.op == "bn":
-                y, st = out
-                if train and st is not None:
-                    a = n.attrs
-                    lay = self.layouts[o]
-                    c = a["channels"]
-                    mean, var = st
-                    nsamp = float(B * math.prod(n.shape) // c)
-                    mom = a["momentum"]
-                    mm = self.stats.narrow(0, lay.mm[n.id], c)
-                    mv = self.stats.narrow(0, lay.mv[n.id], c)
-                    mm.mul_(mom).add_(mean * (1 - mom))
-                    mv.mul_(mom).add_(var * (nsamp / (nsamp - (1 + a["epsilon"]))) * (1 - mom))
-                out = y
-            self._view(mem, o, n.id, inputs, B).copy_(out.to(torch.bfloat16))
-        return fn
-
-    def _fallback_bwd(self, mem, o, n, inputs, B, target, written):
-        tgs = []
-        for i in n.inputs:
-            own = target(o, i)
-            tgs.append(None if own is None else (own, own in written[o]))
-            if own is not None:
-                written[o].add(own)
-        lay = self.layouts[o]
-
-        def fn():
-            xs = [self._view(mem, o, i, inputs, B).float().requires_grad_(True) for i in n.inputs]
-            params = []
-            if n.op == "bn":
-                c = n.attrs["channels"]
-                for d in (lay.gamma, lay.beta):
-                    if n.id in d:
-                        params.append(self.p.narrow(0, d[n.id], c).detach().clone().requires_grad_(True))
-            with torch.enable_grad():
-                out = self._fallback_compute_params(o, n, xs, params)
-                dy = self._view(mem, o, n.id, inputs, B, grad=True).float()
-                grads = torch.autograd.grad(out, xs + params, dy, allow_unused=True)
-            for x_i, gi, tg in zip(n.inputs, grads[:len(xs)], tgs):
-                if tg is None or gi is None:
-                    continue
-                own, acc = tg
-                rec = mem["orgs"][o]
-                dst = mem["grad"].t.narrow(0, (mem["grad"].ptr(rec["grad"][own]) - mem["grad"].t.data_ptr()) // 2,
-                                           gi.numel())
-                g = gi.reshape(-1)
-                if g.numel() != dst.numel():
-                    # broadcast-reduced operand
-                    g = gi.sum_to_size(self._view(mem, o, own, inputs, B).shape).reshape(-1)
-                if acc:
-                    dst.copy_((dst.float() + g).to(torch.bfloat16))
-                else:
-                    dst.copy_(g.to(torch.bfloat16))
-            k = len(xs)
-            if n.op == "bn":
-                c = n.attrs["channels"]
-                for d in (lay.gamma, lay.beta):
-                    if n.id in d:
-                        gg = grads[k]
-                        k += 1
-                        if gg is not None:
-                            self.g.narrow(0, d[n.id], c).add_(H.to_q32(gg))
-        return fn
-
-    def _fallback_compute_params(self, o, n, xs, params):
-        if n.op != "bn":
-            return self._fallback_compute(o, n, xs, True)
-        a = n.attrs
-        lay = self.layouts[o]
-        x = xs[0]
-        ax = a["axis"]
-        red = [i for i in range(x.dim()) if i != ax]
-        shp = [1] * x.dim()
-        shp[ax] = a["channels"]
-        mean = x.mean(red)
-        var = x.var(red, unbiased=False)
-        y = (x - mean.view(shp)) / torch.sqrt(var.view(shp) + a["epsilon"])
-        k = 0
-        if n.id in lay.gamma:
-            y = y * params[k].view(shp)
-            k += 1
-        if n.id in lay.beta:
-            y = y + params[k].view(shp)
-        return y
 
     # ---------------------------------------------------------------------------------------------
     # execution
@@ -1510,7 +1459,6 @@ class HipPopulationEngine(PopulationEngine):
         xb = _padded_zeros((B, xcols), torch.bfloat16, dev)
         gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
         yb = torch.zeros(B, dtype=torch.int32, device=dev)
-        self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
         perm_t = torch.zeros(max(split, 1), dtype=torch.int32, device=dev)
         counter = torch.zeros(1, dtype=torch.int32, device=dev)
         metrics = torch.zeros(P, 4, dtype=torch.int64, device=dev)      # Q32 fixed point (aux.hip loss_kernel)
@@ -1654,6 +1602,8 @@ class HipPopulationEngine(PopulationEngine):
         torch.cuda.synchronize(dev)
         self._train_mem = mem
         self.graph = graph
+        # every buffer the captured graph addresses lives as long as the graph does
+        self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem_plans)
         return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
                          extra={"plan_s": self.timings["plan_s"], "launches_per_step": self.timings["launches_per_step"]})
 
@@ -1677,7 +1627,6 @@ class HipPopulationEngine(PopulationEngine):
         xb = H.padded(torch.as_tensor(np.ascontiguousarray(x.reshape(B, -1)), dtype=torch.float32, device=dev).to(torch.bfloat16))
         gb = H.padded(torch.as_tensor(np.ascontiguousarray(g), dtype=torch.float32, device=dev).to(torch.bfloat16))
         yb = H.padded(torch.as_tensor(y.astype(np.int32), device=dev))
-        self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
         metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
         mem = self._alloc_buffers(B, with_grads=True)
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
@@ -1722,7 +1671,6 @@ class HipPopulationEngine(PopulationEngine):
             gb = _padded_zeros((B, gcols), torch.bfloat16, dev)
             yb = torch.zeros(B, dtype=torch.int32, device=dev)
             metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
-            self._input_tensors.update({xb.data_ptr(): xb, gb.data_ptr(): gb})
             mem = getattr(self, "_train_mem", None)
             if mem is None or mem["B"] != B:
                 mem = self._alloc_buffers(B, with_grads=False)
@@ -1769,9 +1717,6 @@ class HipPopulationEngine(PopulationEngine):
             L = self.layouts[0].ir.genotype_size
             xs = _padded_zeros((P, B, xcols), torch.bfloat16, dev)
             gs = _padded_zeros((P, B, L), torch.bfloat16, dev)
-            for i in range(P):
-                self._input_tensors[xs[i].data_ptr()] = xs[i]
-                self._input_tensors[gs[i].data_ptr()] = gs[i]
             mem = self._alloc_buffers(B, with_grads=False)
             inputs = [{"X": xs[i].data_ptr(), "g": gs[i].data_ptr()} for i in range(P)]
             plan = self._build_plan("infer", B, mem, inputs)
@@ -1805,7 +1750,7 @@ class HipPopulationEngine(PopulationEngine):
                                                dtype=torch.float32, device=dev).to(torch.bfloat16)
             rp["plan"].run()
             if packed:
-                self.lib.rep_bits(rp["descs"].data_ptr(), P, B, H.stream_handle())
+                self.lib.rep_bits(rp["descs"].data_ptr(), P, B, (L + 7) // 8, H.stream_handle())
                 outs.append(rp["bits"][:, :nb].clone())
             else:
                 mem = rp["mem"]
@@ -1844,10 +1789,9 @@ class HipPopulationEngine(PopulationEngine):
             torch.cuda.synchronize(self.device)
         self.graph = None
         self.plans.clear()
-        for name in ("_train_mem", "_train_mem_rem", "_debug_mem", "_adam_skip", "_adam_ctx", "_streams"):
+        for name in ("_fit_bufs", "_train_mem", "_train_mem_rem", "_debug_mem", "_adam_skip", "_adam_ctx", "_streams"):
             if hasattr(self, name):
                 delattr(self, name)
-        self._input_tensors = {}
 
 
 def device_data_for_arrays(x, labels, g, device):

@@ -33,7 +33,7 @@ import pandas as pd
 
 from ..genome.interpreter import layer_counts
 from ..parallel.comm import Comm, LocalComm, pack_header, unpack_results
-from ..parallel.partition import lpt_partition
+from ..parallel.partition import RankSpeedModel, lpt_partition
 from ..utils.faults import GenerationWatchdog, job_scale, maybe_inject
 from ..utils.levenshtein import levenshtein_batch
 from ..utils.stats import fertility, genotype_stats, source_code_stats
@@ -72,6 +72,8 @@ class Experiment:
                                      int(parameters["genotype_size"]),
                                      int(parameters["num_classification_classes"]))
         self.history: List[dict] = []
+        # per-rank speed factors learned from measured shard times (replicated: every rank updates the same)
+        self._speeds = RankSpeedModel(self._comm.world_size)
         if job_timeout is None:
             # the reference pool's per-job timeout (config.py:7), armed by default only where a stall is
             # plausible and recoverable: the GPU engine, or a run under the supervising launcher.  A slow
@@ -162,6 +164,10 @@ class Experiment:
                           mean_val_acc=float(np.nanmean(current["classification_validation_accuracy"]))
                           if len(valid_serann) else float("nan"),
                           stats_db_seconds=t_db - t_stats)
+            if self._comm.world_size > 1:
+                ms = [v for v in times["rank_measured_s"] if v > 0]
+                record["rank_imbalance"] = max(ms) / (sum(ms) / len(ms)) if ms else float("nan")
+                record["rank_factors"] = times["rank_factors"]
 
             if len(valid_serann) == 0:
                 self.log("No valid SeRANNs left! stopping...")
@@ -253,7 +259,7 @@ class Experiment:
         sources = list(current["source_code"])
         comm = self._comm
         plan = plan_generation(sources, self._cache, float(p["max_serann_parameters"]), comm)
-        parts = lpt_partition(plan.costs, comm.world_size, plan.arch_keys)
+        parts = lpt_partition(plan.costs, comm.world_size, plan.arch_keys, speeds=self._speeds.factors)
         local = [int(plan.trainable[i]) for i in parts[comm.rank]]
         # the shard is this many reference pool jobs: give the watchdog that many job timeouts
         self._watchdog.arm(f"generation {generation}", job_scale(len(local)))
@@ -274,14 +280,19 @@ class Experiment:
         metrics = np.full((n, 4), np.nan)
         offspring_rows: Dict[int, np.ndarray] = {}
         times = {"learning_times": [], "replication_times": [], "train_flops": self._train_flops(plan)}
-        for blob in gathered:
+        measured = []
+        for blob in gathered:                        # rank order
             idx, m, off, lt, rt = unpack_results(blob)
+            measured.append(float(lt) if len(idx) else 0.0)
             if len(idx):
                 metrics[idx] = m
                 for k, i in enumerate(idx):
                     offspring_rows[int(i)] = off[k]
                 times["learning_times"].append(lt)
                 times["replication_times"].append(rt)
+        predicted = [float(sum(plan.costs[j] for j in part)) for part in parts]
+        times["rank_predicted_s"], times["rank_measured_s"] = predicted, measured
+        times["rank_factors"] = self._speeds.update(predicted, measured)
 
         models_info = pd.DataFrame(index=current.index)
         models_info["parameters_count"] = [r.parameters_count for r in plan.results]

@@ -29,6 +29,10 @@ BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "m
 POOL_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "idx", "dy", "dx", "B", "H", "W", "C", "OH", "OW", "PH", "PW",
                                          "SH", "SW", "flags"]])
 COPY_DTYPE = np.dtype([(f, _I) for f in ["src", "dst", "rows", "cols", "src_stride", "dst_stride", "flags"]])
+EW_DTYPE = np.dtype([("a", _I), ("b", _I), ("out", _I), ("D", _I, (4,)), ("R", _I, (4,)), ("aJ", _I, (4,)),
+                     ("aR", _I, (4,)), ("bJ", _I, (4,)), ("bR", _I, (4,)), ("ca", np.float32), ("cb", np.float32),
+                     ("c", np.float32), ("pad", np.float32), ("flags", _I)])
+EW_ELEMS = 2048        # ew.hip: destination elements per block
 SPLITFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "bias", "M", "N", "S", "act", "flags"]])
 SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kernel
 CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy", "dw", "dbias", "B", "H", "W", "F",
@@ -300,13 +304,73 @@ def available() -> bool:
 
 def check_layouts():
     sizes = lib().desc_sizes()
-    for name, dt in [("GemmDesc", GEMM_DTYPE), ("BnDesc", BN_DTYPE),
+    for name, dt in [("GemmDesc", GEMM_DTYPE), ("BnDesc", BN_DTYPE), ("EwDesc", EW_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
                      ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE), ("AdamCtx", ADAM_CTX_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
+
+
+# ---- strided elementwise rows (ew.hip): the interpreter's rare ops --------------------------------------
+def _pad4(v, fill):
+    v = [int(x) for x in v]
+    if len(v) > 4:
+        raise ValueError(f"ew: rank {len(v)} > 4")
+    return [fill] * (4 - len(v)) + v
+
+
+def _dense_strides(shape):
+    st, acc = [], 1
+    for d in reversed([int(x) for x in shape]):
+        st.append(acc)
+        acc *= d
+    return list(reversed(st))
+
+
+def _bcast_strides(src_shape, shape):
+    """Element strides reading a dense ``src_shape`` tensor broadcast to ``shape`` (same rank)."""
+    if len(src_shape) != len(shape):
+        raise ValueError("ew: broadcast operands need equal ranks")
+    st = _dense_strides(src_shape)
+    return [0 if int(s) == 1 and int(d) != 1 else st[k] for k, (s, d) in enumerate(zip(src_shape, shape))]
+
+
+def ew_map_row(out, shape, a, a_shape, ca=1.0, b=0, b_shape=None, cb=0.0, c=0.0, accum=False) -> dict:
+    """out[shape] (+)= ca * A + cb * B + c, A / B dense tensors of ``a_shape`` / ``b_shape`` broadcast to
+    ``shape`` (full shapes, batch included).  Row for EW_DTYPE; count = ew_count(row)."""
+    one = [1, 1, 1, 1]
+    return dict(a=a, b=b, out=out, D=_pad4(shape, 1), R=one, aJ=_pad4(_bcast_strides(a_shape, shape), 0),
+                aR=[0] * 4, bJ=_pad4(_bcast_strides(b_shape, shape), 0) if b else [0] * 4, bR=[0] * 4,
+                ca=float(ca), cb=float(cb), c=float(c), pad=0.0, flags=1 if accum else 0)
+
+
+def ew_reduce_row(out, out_shape, src, src_shape, scale=1.0, accum=False) -> dict:
+    """out[out_shape] (+)= scale * (src summed over the dimensions where ``out_shape`` is 1 and
+    ``src_shape`` is not): the gradient of an operand broadcast to ``src_shape``."""
+    st = _dense_strides(src_shape)
+    red = [int(o) == 1 and int(s) != 1 for o, s in zip(out_shape, src_shape)]
+    return dict(a=src, b=0, out=out, D=_pad4(out_shape, 1),
+                R=_pad4([int(s) if r else 1 for s, r in zip(src_shape, red)], 1),
+                aJ=_pad4([0 if r else st[k] for k, r in enumerate(red)], 0),
+                aR=_pad4([st[k] if r else 0 for k, r in enumerate(red)], 0),
+                bJ=[0] * 4, bR=[0] * 4, ca=float(scale), cb=0.0, c=0.0, pad=0.0, flags=1 if accum else 0)
+
+
+def ew_permute_row(out, src, dims, perm, accum=False) -> dict:
+    """out (dense, dims permuted by ``perm``) (+)= src (dense ``dims``): out[i_perm] = src[i]."""
+    st = _dense_strides(dims)
+    return dict(a=src, b=0, out=out, D=_pad4([dims[p] for p in perm], 1), R=[1, 1, 1, 1],
+                aJ=_pad4([st[p] for p in perm], 0), aR=[0] * 4, bJ=[0] * 4, bR=[0] * 4,
+                ca=1.0, cb=0.0, c=0.0, pad=0.0, flags=1 if accum else 0)
+
+
+def ew_count(row) -> int:
+    n = 1
+    for d in row["D"]:
+        n *= int(d)
+    return -(-n // EW_ELEMS)
 
 
 OPERAND_SLACK_BYTES = 256   # readable memory every kernel operand must have behind its last element

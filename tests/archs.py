@@ -57,6 +57,17 @@ ARCHS = {
         "g_layer = g_layer-1\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
         "con = Dense(units=20, activation='relu')(con)\nloss_balance = 0.4"),
+    # BatchNormalization on non-last axes (of a conv output and of a genotype feature map) and a broadcasting
+    # tensor - tensor subtraction: ew.hip transposes / maps / broadcast-gradient reductions
+    "mutant_bn_axis_bsub": (
+        "X_layer = Conv2D(filters=8, kernel_size=3, strides=2)(X_layer)\n"
+        "X_layer = BatchNormalization(axis=1)(X_layer)\n"
+        "g_layer = Dense(units=16, activation='relu')(g_layer)\n"
+        "con = Dense(units=1)(g_layer)\n"
+        "g_layer = g_layer-con\n"
+        "g_layer = BatchNormalization(axis=-2)(g_layer)\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n"
+        "con = Dense(units=20, activation='relu')(con)\nloss_balance = 0.4"),
     "conv1d_rank4_and_strided_pool": (
         "X_layer = Conv2D(filters=8, kernel_size=3, strides=1)(X_layer)\n"
         "X_layer = Conv1D(filters=8, kernel_size=3, strides=2)(X_layer)\n"

@@ -47,35 +47,6 @@ def _oracle(ir, params, x, g, y):
     return logits, grads
 
 
-@pytest.mark.parametrize("name", sorted(ARCHS))
-def test_train_step_matches_oracle(name):
-    from serann.engine.hip_engine import HipPopulationEngine
-    ir = interpret(ARCHS[name])
-    params = init_params(ir, 7)
-    x, g, y = _batch(96)
-    eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
-    grads, metrics = eng.debug_train_step(x, g, y)
-    logits = eng.debug_logits()[0]
-    ref_logits, ref_grads = _oracle(ir, params, x, g, y)
-    assert _rel(logits, ref_logits) < 3e-2, _rel(logits, ref_logits)
-    hip_grads = eng.export_arena(0, grads)
-    for nid, d in ref_grads.items():
-        for k, v in d.items():
-            got = hip_grads[nid][k]
-            if np.linalg.norm(v) < 1e-5:
-                # mathematically ~0 (e.g. the bias of a layer feeding BatchNormalization): only the
-                # bf16 rounding noise of the HIP path remains -> absolute check
-                assert np.linalg.norm(got) < 2e-2, (name, nid, k, np.linalg.norm(got))
-                continue
-            # a gradient that nearly cancels (|v| < 2 % of its layer's kernel gradient, e.g. the bias of a
-            # Conv1D under a sigmoid Dense + BatchNormalization) is judged on the layer's scale
-            scale = 0.02 * np.linalg.norm(d["kernel"]) if "kernel" in d else 0.0
-            err = np.linalg.norm(np.asarray(got, np.float64) - v) / max(np.linalg.norm(v), scale, 1e-12)
-            cos = float(np.dot(got.ravel(), v.ravel()) / (np.linalg.norm(got) * np.linalg.norm(v) + 1e-30))
-            assert err < 0.2 and (cos > 0.98 or np.linalg.norm(v) < scale), (name, nid, k, err, cos)
-    assert metrics[0, 3] == 96
-
-
 def _oracle_dev(ir, params, x, g, y, device, dtype):
     org = Organism(ir, params, device=device, dtype=dtype)
     xb = torch.as_tensor(x, device=device, dtype=dtype)
@@ -92,18 +63,11 @@ def _oracle_dev(ir, params, x, g, y, device, dtype):
     return grads
 
 
-@pytest.mark.parametrize("name", sorted(ARCHS))
-def test_train_step_b750_as_accurate_as_torch_bf16(name):
-    """Production batch (750): every gradient of the HIP engine is within 1.5x (+1 %) of the error that
-    PyTorch's own bf16 computation of the same organism (bf16 GEMM operands on the GPU) makes against the
-    fp32 CPU oracle, and the logits within 1 % of the oracle.  Sums that cancel to ~1e-5 of their terms
-    (the beta of a BatchNormalization on the raw image: sum dy ~ 3e-5 of sum |dy|) keep an absolute floor
-    of 0.1 % of the largest gradient element: the engine stores activations in bf16 (the torch reference
-    keeps them fp32), so such a sum is bf16 noise in the engine (scripts/debug_bn_input.py)."""
+def _check_vs_torch_bf16(name, B, seed):
     from serann.engine.hip_engine import HipPopulationEngine
     ir = interpret(ARCHS[name])
     params = init_params(ir, 7)
-    x, g, y = _batch(750, seed=2)
+    x, g, y = _batch(B, seed=seed)
     eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
     grads, metrics = eng.debug_train_step(x, g, y)
     ref_logits, ref = _oracle(ir, params, x, g, y)
@@ -118,11 +82,30 @@ def test_train_step_b750_as_accurate_as_torch_bf16(name):
             floor = 1e-3 * gmax * np.sqrt(v.size)
             if k == "bias" and "kernel" in d:
                 # the bias of a layer feeding a BatchNormalization has a mathematically zero gradient; the
-                # engine's sum of bf16 BN dx over 588k rows leaves noise on the layer's scale (as the
+                # engine's sum of bf16 BN dx over the batch leaves noise on the layer's scale (as the
                 # reference's pure-fp16 Keras does)
                 floor = max(floor, 0.02 * np.linalg.norm(d["kernel"]))
-            assert a_h < 1.5 * a_b + 0.01 * np.linalg.norm(v) + floor, (name, nid, k, a_h, a_b, np.linalg.norm(v))
-    assert metrics[0, 3] == 750
+            assert a_h < 1.5 * a_b + 0.01 * np.linalg.norm(v) + floor, (name, B, nid, k, a_h, a_b, np.linalg.norm(v))
+    assert metrics[0, 3] == B
+    eng.close()
+
+
+@pytest.mark.parametrize("name", sorted(ARCHS))
+def test_train_step_b750_as_accurate_as_torch_bf16(name):
+    """Production batch (750): every gradient of the HIP engine is within 1.5x (+1 %) of the error that
+    PyTorch's own bf16 computation of the same organism (bf16 GEMM operands on the GPU) makes against the
+    fp32 CPU oracle, and the logits within 1 % of the oracle.  Sums that cancel to ~1e-5 of their terms
+    (the beta of a BatchNormalization on the raw image: sum dy ~ 3e-5 of sum |dy|) keep an absolute floor
+    of 0.1 % of the largest gradient element: the engine stores activations in bf16 (the torch reference
+    keeps them fp32), so such a sum is bf16 noise in the engine (scripts/debug_bn_input.py)."""
+    _check_vs_torch_bf16(name, 750, 2)
+
+
+@pytest.mark.parametrize("name", sorted(ARCHS))
+def test_train_step_b96_as_accurate_as_torch_bf16(name):
+    """The same criterion at a small batch (96 rows: BatchNorm statistics and the loss mean over few rows,
+    remainder-step shapes).  Replaces round 3's loose oracle check (20 % error, cosine 0.98)."""
+    _check_vs_torch_bf16(name, 96, 0)
 
 
 def test_population_grouping_matches_single():

@@ -442,3 +442,42 @@ def test_v3_accumulating_outputs(shape):
                                 K=KH * KW * C, flags=H.GF_ACCUM, **geo)], [(B * OH * OW, Fo, KH * KW * C)])
     ref_y = prev_y.float() + ref_conv2d(xr, wr, None, (SH, SW)).permute(0, 2, 3, 1)
     assert _rel(y.float(), ref_y) < 6e-3
+
+
+def _ew_run(rows):
+    d = _desc(rows, H.EW_DTYPE)
+    t = torch.as_tensor(H.chunk_tiles([H.ew_count(r) for r in rows], 1), device=DEV)
+    H.lib().ew(d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+    torch.cuda.synchronize()
+
+
+def test_ew_map_reduce_permute():
+    """ew.hip (rare ops: neg / broadcasting sub / non-last-axis BatchNormalization transposes) against
+    torch: a broadcast binary map, the gradient reduction of each broadcast operand (with accumulate), and
+    the [outer][C][inner] -> [outer][inner][C] permutation."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    sa, sb = (5, 6, 1, 7), (5, 1, 3, 1)
+    out_shape = (5, 6, 3, 7)
+    a = H.padded(torch.randn(sa, device=DEV, generator=g).bfloat16())
+    b = H.padded(torch.randn(sb, device=DEV, generator=g).bfloat16())
+    y = H.operand(out_shape, torch.bfloat16, DEV)
+    _ew_run([H.ew_map_row(y.data_ptr(), out_shape, a.data_ptr(), sa, ca=1.0, b=b.data_ptr(), b_shape=sb, cb=-1.0, c=0.5)])
+    ref = a.float() - b.float() + 0.5
+    assert _rel(y.float(), ref) < 6e-3
+    # d/da of (a - b) broadcast: sum over the broadcast axis, accumulated onto an existing gradient
+    dy = H.padded(torch.randn(out_shape, device=DEV, generator=g).bfloat16())
+    prev = torch.randn(sa, device=DEV, generator=g).bfloat16()
+    da = H.padded(prev.clone())
+    db = H.operand(sb, torch.bfloat16, DEV)
+    _ew_run([H.ew_reduce_row(da.data_ptr(), sa, dy.data_ptr(), out_shape, 1.0, accum=True),
+             H.ew_reduce_row(db.data_ptr(), sb, dy.data_ptr(), out_shape, -1.0)])
+    assert _rel(da.float(), prev.float() + dy.float().sum(2, keepdim=True)) < 6e-3
+    assert _rel(db.float(), -dy.float().sum((1, 3), keepdim=True)) < 6e-3
+    # neg and the channels-last permutation of a BN over axis 1 of (B, C, H, W)
+    x = H.padded(torch.randn(4, 9, 5, 3, device=DEV, generator=g).bfloat16())
+    xt = H.operand(4 * 5 * 3 * 9, torch.bfloat16, DEV)
+    _ew_run([H.ew_permute_row(xt.data_ptr(), x.data_ptr(), (4, 9, 15), (0, 2, 1))])
+    assert torch.equal(xt.view(4, 15, 9), x.view(4, 9, 15).permute(0, 2, 1))
+    n = H.operand((4, 9, 5, 3), torch.bfloat16, DEV)
+    _ew_run([H.ew_map_row(n.data_ptr(), (4, 9, 5, 3), x.data_ptr(), (4, 9, 5, 3), ca=-1.0)])
+    assert torch.equal(n, -x)
