@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--decode-n", type=int, default=4096)
+    ap.add_argument("--cpu-ref-n", type=int, default=1024, help="genotypes decoded by the fp32 CPU reference")
     ap.add_argument("--train-only", action="store_true",
                     help="stop after the training measurement (profiling: no torch reference decode / encode)")
     ap.add_argument("--engine", default="auto", choices=["auto", "hip", "torch"],
@@ -79,6 +80,20 @@ def main():
     got, dt_dec = timed(lambda: model.decode_tokens(g, device=dev))
     out["decode_genotypes_per_sec"] = a.decode_n / dt_dec
     out["decode_token_agreement_vs_torch"] = float((got == ref).mean())
+    # the parity that matters: the fp32 model on the CPU (no GPU library path involved), on the first
+    # --cpu-ref-n genotypes; and the GPU torch model in 512-genotype chunks (large single batches of the
+    # fp32 nets have returned wrong logits on this ROCm image, see the encode note below)
+    import copy
+    ncpu = min(a.cpu_ref_n, a.decode_n)
+    cpu_model = copy.deepcopy(model).cpu().float().eval()
+    with torch.no_grad():
+        ref_cpu = np.concatenate([cpu_model.decode(torch.as_tensor(g[i:i + 256])).numpy() for i in range(0, ncpu, 256)])
+        ref_chunks = np.concatenate([model.decode(torch.as_tensor(g[i:i + 512], device=dev)).cpu().numpy()
+                                     for i in range(0, a.decode_n, 512)])
+    out["decode_token_agreement_vs_cpu_fp32"] = float((got[:ncpu] == ref_cpu).mean())
+    out["decode_token_agreement_vs_torch_512_chunks"] = float((got == ref_chunks).mean())
+    out["torch_gpu_vs_cpu_fp32_agreement"] = float((ref_chunks[:ncpu] == ref_cpu).mean())
+    out["decode_cpu_ref_genotypes"] = int(ncpu)
     # encode (K30-K32, K35): token sequences -> genotype bits on the HIP path
     toks = seqs[np.random.default_rng(1).integers(0, len(seqs), a.decode_n)]
     # torch reference in chunks of 512: on this ROCm image the fp32 inference net on one 4096-sequence

@@ -11,6 +11,10 @@
 #   bench1                  one 1-GPU bench run
 #   pop50                   BASELINE config #2: pop 50, example.json, 1 GPU
 #   evaluation              seconds per evaluated genotype
+#   pop50long               BASELINE config #2 at its real length: run_experiment CLI, example.json, 100 generations
+#   evalgeneral             BASELINE config #5: run_evaluation CLI (E = 5, R = 100, general sampler) over ~300
+#                           genotypes of the pop50long experiment; dies after its first 100 pickled results
+#                           (fault injection, exit 75) and is relaunched, resuming from the pickle
 mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
 R=$(pwd)
@@ -22,6 +26,10 @@ run() {
   echo "rc=$rc" | tee -a gpurun_out/session.log
   tail -4 "gpurun_out/$name.log" | cut -c1-600 | tee -a gpurun_out/session.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step $name failed (rc=$rc), stopping"; exit $rc; fi
+  # a failing test run (rc 1) may hide a GPU fault caught as an exception: nothing more runs on the GPU then
+  if grep -qE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
+    echo "step $name hit a GPU fault, stopping" | tee -a gpurun_out/session.log; exit 3
+  fi
   return 0
 }
 stats() {   # keep the kernel statistics of a rocprofv3 run, drop the (large) traces
@@ -56,4 +64,29 @@ has calib && run calib 900 python scripts/calibrate_cost.py --population-file po
 has bench1 && run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
 has pop50 && run pop50 600 python bench.py --gpus 1 --pop-per-gpu 50 --parameters serann/parameters/experiment/example.json --steps ${BSTEPS:-3} --warmup 1
 has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
+
+export SERANN_EXPERIMENT_RESULTS_DIR=$R/gpurun_out/ev/exp
+export SERANN_SERANN_EVALUATIONS_DIR=$R/gpurun_out/ev/evals
+if has pop50long; then
+  mkdir -p gpurun_out/ev/exp
+  run pop50long 1100 python -u evolutionary_experiment/run_experiment.py -p serann/parameters/experiment/example.json \
+      --perf-log gpurun_out/ev/pop50_100gen.jsonl
+fi
+if has evalgeneral; then
+  db=$(ls gpurun_out/ev/exp/*.sqlite | head -1)
+  eid=$(basename "$db" .sqlite)
+  python - "$eid" <<'PY'
+import json, sys
+p = json.load(open("serann/parameters/evaluation/general.json"))
+p.update(experiment_id=sys.argv[1], generation_step=1, samples_per_generation=3)
+json.dump(p, open("gpurun_out/ev/general_r4.json", "w"), indent=1)
+PY
+  echo "=== evalgeneral_cut ===" | tee -a gpurun_out/session.log
+  SERANN_FAULT_INJECT=evaluated=100,mode=exit timeout -k 10 900 python -u serann_evaluation/run_evaluation.py \
+      -p gpurun_out/ev/general_r4.json -n general_r4 > gpurun_out/evalgeneral_cut.log 2>&1
+  rc=$?
+  echo "rc=$rc (75 = the injected death after the first pickle)" | tee -a gpurun_out/session.log
+  if [ $rc -ne 75 ] && [ $rc -ne 0 ]; then echo "evalgeneral_cut failed (rc=$rc), stopping"; exit $rc; fi
+  run evalgeneral 900 python -u serann_evaluation/run_evaluation.py -p gpurun_out/ev/general_r4.json -n general_r4
+fi
 exit 0

@@ -70,12 +70,22 @@ def build_hip(jobs: int = 4):
     objs = []
 
     hdr_mtime = max((h.stat().st_mtime for h in (CSRC / "hip").glob("*.h")), default=0.0)
+    # the sources' digest goes into module.hip (src_hash()); the loader checks it against the tree
+    sys.path.insert(0, str(PKG))
+    from utils.native import hip_source_hash
+    sys.path.pop(0)
+    digest = hip_source_hash(CSRC / "hip")
+    stamp = build_dir / "src_hash.txt"
+    stale_digest = not stamp.exists() or stamp.read_text().strip() != digest
 
     def compile_one(src):
         obj = build_dir / (src.stem + ".o")
         extra = PER_FILE_FLAGS.get(src.name, [])
+        if src.name == "module.hip":
+            extra = extra + [f'-DSERANN_SRC_HASH="{digest}"']
         # incremental: an object newer than its source and every header is reused
-        if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_mtime):
+        if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hdr_mtime) and not (
+                src.name == "module.hip" and stale_digest):
             return obj
         _run([hipcc, *flags, *extra, "-c", str(src), "-o", str(obj)])
         return obj
@@ -84,6 +94,7 @@ def build_hip(jobs: int = 4):
         objs = list(ex.map(compile_one, srcs))
     out = NATIVE / f"serann_hip{_ext_suffix()}"
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", *map(str, objs), "-o", str(out)])
+    stamp.write_text(digest)
     return out
 
 

@@ -7,6 +7,10 @@
 
 namespace py = pybind11;
 
+#ifndef SERANN_SRC_HASH
+#define SERANN_SRC_HASH "unknown"
+#endif
+
 static py::dict desc_sizes() {
     py::dict d;
     d["GemmDesc"] = sizeof(GemmDesc);
@@ -29,6 +33,7 @@ static py::dict desc_sizes() {
 PYBIND11_MODULE(serann_hip, m) {
     m.doc() = "SeRANN-AMD HIP/CDNA4 kernels (gfx950)";
     m.def("desc_sizes", &desc_sizes);
+    m.def("src_hash", []() { return std::string(SERANN_SRC_HASH); });
     m.def("gemm3", &launch_gemm3, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
           py::arg("ntiles"), py::arg("stream"));
     m.def("transpose_weights", &launch_transpose_weights);

@@ -66,11 +66,11 @@ __device__ __forceinline__ float nbn_y(const float* xr, const float* w, float b,
 }  // namespace
 
 template <int PHASE, int K>
-__global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ descs, const int2* __restrict__ tiles) {
+__global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ descs, const int4* __restrict__ tiles) {
     constexpr int NQ = PHASE == 5 ? K + 1 : (PHASE == 4 ? 2 : 1);   // reduced quantities per element slot
     __shared__ float red[NQ * 2048];
     __shared__ float pa[256], pb[256], pc[256];
-    const int2 td = tiles[blockIdx.x];
+    const int4 td = tiles[blockIdx.x];       // (problem, first super-row, end super-row, first-block flag)
     const NbnDesc& d = descs[td.x];
     const int R = (int)d.R, F = (int)d.F, act = (int)d.act, ldx = (int)d.ldx;
     const int flags = (int)d.flags;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
             const float gsc = (flags & 1) ? gamma[f] * is : is;
             a = gsc;
             b = ((flags & 2) ? beta[f] : 0.f) - mu * gsc;
-            if (td.y == 0) {
+            if (td.w) {
                 const float mom = (float)d.momentum;
                 float* mm = reinterpret_cast<float*>(d.mm);
                 float* mv = reinterpret_cast<float*>(d.mv);
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
             a = gg;                                   // k1
             b = -gg * is * mb;                        // k2
             e = -gg * (ma - mu * is * mb);            // k3
-            if (td.y == 0) {                          // BN parameter gradients, once per problem
+            if (td.w) {                               // BN parameter gradients, once per problem
                 if (flags & 1) reinterpret_cast<long long*>(d.dgamma)[f] += fx_q(sdyx);
                 if (flags & 2) reinterpret_cast<long long*>(d.dbeta)[f] += fx_q(sdy);
             }
@@ -147,9 +147,9 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
 #pragma unroll
     for (int j = 0; j < 8 * NQ; ++j) acc[j] = 0.f;
 
+    // super-row range of this block: chosen by the planner (hip_ops.nbn_tiles), a function of the problem
     const int nsr = (R + 7) / 8;
-    const int srb = nbn_super_rows(F, PHASE);
-    const int sr0 = td.y * srb, sr1 = min(nsr, sr0 + srb);
+    const int sr0 = td.y, sr1 = min(nsr, td.z);
     const int64_t total = (int64_t)R * F;
     const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.dy);
     bf16_t* __restrict__ Yo = reinterpret_cast<bf16_t*>(d.y);
@@ -273,7 +273,7 @@ void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles
     const dim3 grid((unsigned)ntiles), block(256);
     hipStream_t s = as_stream(stream);
     const NbnDesc* dp = as_ptr<const NbnDesc>(descs);
-    const int2* tp = as_ptr<const int2>(tiles);
+    const int4* tp = as_ptr<const int4>(tiles);
 #define NBN_CASE(P_, K_) \
     if (phase == P_ && k == K_) { hipLaunchKernelGGL((nbn_kernel<P_, K_>), grid, block, 0, s, dp, tp); return; }
 #define NBN_K(K_) NBN_CASE(2, K_) NBN_CASE(4, K_) NBN_CASE(5, K_)

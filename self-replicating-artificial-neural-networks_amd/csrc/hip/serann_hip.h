@@ -139,12 +139,8 @@ struct NbnDesc {
     int64_t R, F, K, ldx, act, flags;
     double eps, momentum;
 };
-constexpr int NBN_ELEMS = 16384;       // elements per block of phase 2
-constexpr int NBN_RED_MULT = 4;        // phases 4 / 5 (block reductions) take 4x the rows per block
-__host__ __device__ inline int nbn_super_rows(int F, int phase) {
-    const int s1 = (NBN_ELEMS / 8) / F > 1 ? (NBN_ELEMS / 8) / F : 1;
-    return phase == 2 ? s1 : s1 * NBN_RED_MULT;
-}
+// nbn tiles (int4): (problem, first super-row, end super-row, 1 for the problem's first block); the planner
+// sizes the ranges (hip_ops.nbn_tiles)
 void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float b2, uint64_t stream);
 void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
                         float b1, float b2, float eps, uint64_t skip, uint64_t stream);

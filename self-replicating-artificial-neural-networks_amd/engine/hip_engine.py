@@ -891,8 +891,10 @@ class HipPopulationEngine(PopulationEngine):
                 by_k.setdefault(int(r["K"]), []).append(r)
             for k_ in sorted(by_k):
                 rws = by_k[k_]
-                add_chunked("nbn", (phase, k_), rws, H.NBN_DTYPE,
-                            [H.nbn_chunks(r["R"], r["F"], phase) for r in rws], 1)
+                tiles = H.nbn_tiles([(r["R"], r["F"]) for r in rws], phase)
+                if len(tiles):
+                    plan.launches.append(Launch("nbn", (phase, k_), desc_tensor(rws, H.NBN_DTYPE), T(tiles),
+                                                len(tiles)))
 
         # gemm node -> the (first) last-axis BatchNormalization reading its output with matching channels
         bn_consumer = [dict() for _ in range(P)]

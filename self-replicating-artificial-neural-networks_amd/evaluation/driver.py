@@ -23,6 +23,7 @@ import numpy as np
 import pandas as pd
 
 from ..parallel.comm import Comm, LocalComm
+from ..utils.faults import maybe_inject_evaluation
 
 SAMPLERS: Dict[str, type] = {}
 
@@ -92,13 +93,14 @@ class GeneralSampler(SamplerInterface):
 
 class SampleDeepEvaluator:
     def __init__(self, experiment_df: pd.DataFrame, output_path: str, sample_ids, worker, comm: Optional[Comm] = None,
-                 shared_cache: bool = True, batch: int = 4, log=print):
+                 shared_cache: bool = True, batch: int = 4, log=print, save_every: int = 100):
         self.comm = comm or LocalComm()
         self._exp_df = experiment_df
         self._output_path = str(output_path)
         self._shared = shared_cache
         self.worker = worker
         self.batch = max(1, int(batch))
+        self.save_every = max(1, int(save_every))       # results between pickles (reference: 100)
         self.log = log if self.comm.is_root else (lambda *a, **k: None)
         sample_ids = list(pd.Index(sample_ids).drop_duplicates())
         if Path(self._output_path).is_file():
@@ -157,9 +159,11 @@ class SampleDeepEvaluator:
             avg = float(np.mean(durations[-200:]))
             self.log(f"{done}/{len(remaining)} jobs done. Average evaluation time: {int(avg) // 60:02d}:"
                      f"{int(avg) % 60:02d}.")
-            if comm.is_root and (done // 100 != (done - sum(len(p) for p in gathered)) // 100 or k == rounds - 1):
+            se = self.save_every
+            if comm.is_root and (done // se != (done - sum(len(p) for p in gathered)) // se or k == rounds - 1):
                 self.log("Saving to disk.")
                 self.save()
+                maybe_inject_evaluation(sum(1 for r in self._results.values() if len(r)), comm.rank)
         if comm.is_root and rounds == 0:
             self.save()
         return self._results

@@ -112,14 +112,36 @@ BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256
 NBN_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "dy", "gamma", "beta", "mm", "mv", "mean", "invstd",
                                         "ws", "wsb", "dw", "db", "dgamma", "dbeta", "R", "F", "K", "ldx", "act",
                                         "flags"]] + [("eps", np.float64), ("momentum", np.float64)])
-NBN_ELEMS, NBN_RED_MULT = 16384, 4     # serann_hip.h nbn_super_rows
+# nbn.hip block sizes: elements per block of phase 2 (a streaming write; each block first rebuilds the
+# per-channel scale / shift from the statistics workspace, so short blocks pay that prologue often), and
+# the multiple of it taken by the reduction phases 4 / 5
+NBN_ELEMS = int(_os.environ.get("SERANN_NBN_ELEMS", "16384"))
+NBN_RED_MULT = int(_os.environ.get("SERANN_NBN_RED_MULT", "4"))
+
+
+def nbn_super_rows(units: int, phase: int) -> int:
+    """Super-rows (8 rows) per nbn block: a function of the problem alone (the phase 4 / 5 block partial
+    sums meet in fixed point, so their boundaries fix the rounding)."""
+    s1 = max(1, (NBN_ELEMS // 8) // int(units))
+    return s1 if phase == 2 else s1 * NBN_RED_MULT
 
 
 def nbn_chunks(rows: int, units: int, phase: int) -> int:
     """Blocks of a fused raw-input Dense -> BatchNormalization problem [rows][units] (nbn.hip)."""
-    s1 = max(1, (NBN_ELEMS // 8) // int(units))
-    srb = s1 if phase == 2 else s1 * NBN_RED_MULT
-    return -(-(-(-int(rows) // 8)) // srb)
+    return -(-(-(-int(rows) // 8)) // nbn_super_rows(units, phase))
+
+
+def nbn_tiles(rows_units, phase: int) -> np.ndarray:
+    """int32 (ntiles, 4) tile table of one nbn launch: (problem, first super-row, end super-row, first flag)
+    for problems of (rows, units)."""
+    out = []
+    for p, (rows, units) in enumerate(rows_units):
+        nsr = -(-int(rows) // 8)
+        srb = nbn_super_rows(units, phase)
+        s0 = np.arange(0, nsr, srb)
+        if len(s0):
+            out.append(np.stack([np.full(len(s0), p), s0, np.minimum(nsr, s0 + srb), (s0 == 0).astype(int)], 1))
+    return np.concatenate(out).astype(np.int32) if out else np.zeros((0, 4), np.int32)
 
 
 BN_RED_MULT = 4        # aux.hip: the statistics phases (0, 4) take BN_RED_MULT x the rows per block

@@ -11,6 +11,7 @@ test (or an operator rehearsing a rank loss) kill a rank at a chosen generation:
     SERANN_FAULT_INJECT="generation=2,rank=1,mode=exit"  # rank 1 exits with status 75 (simulated death)
 
     SERANN_FAULT_INJECT="generation=2,mode=hang"       # every rank stalls (the watchdog must fire)
+    SERANN_FAULT_INJECT="evaluated=100,mode=exit"      # run_evaluation dies after its first saved 100 results
 
 The fault fires at the start of the generation, before any training or DB write of it, so the DB
 holds exactly the generations before it.
@@ -42,14 +43,15 @@ class InjectedFault(RuntimeError):
 def parse(spec: Optional[str]) -> Optional[dict]:
     if not spec:
         return None
-    out = {"generation": None, "rank": None, "mode": "raise"}
+    out = {"generation": None, "evaluated": None, "rank": None, "mode": "raise"}
     for item in spec.split(","):
         key, _, val = item.strip().partition("=")
         if key not in out or not val:
-            raise ValueError(f"{ENV}: bad item {item!r} (expected generation=G[,rank=R][,mode=raise|exit|hang])")
+            raise ValueError(f"{ENV}: bad item {item!r} (expected generation=G|evaluated=N[,rank=R]"
+                             f"[,mode=raise|exit|hang])")
         out[key] = val if key == "mode" else int(val)
-    if out["generation"] is None:
-        raise ValueError(f"{ENV}: generation=G is required")
+    if (out["generation"] is None) == (out["evaluated"] is None):
+        raise ValueError(f"{ENV}: exactly one of generation=G, evaluated=N is required")
     if out["mode"] not in ("raise", "exit", "hang"):
         raise ValueError(f"{ENV}: mode must be raise, exit or hang")
     return out
@@ -57,14 +59,28 @@ def parse(spec: Optional[str]) -> Optional[dict]:
 
 def maybe_inject(generation: int, rank: int = 0, spec: Optional[str] = None) -> None:
     f = parse(os.environ.get(ENV) if spec is None else spec)
-    if f is None or f["generation"] != int(generation) or (f["rank"] is not None and f["rank"] != int(rank)):
+    if f is None or f["generation"] is None or f["generation"] != int(generation) or \
+            (f["rank"] is not None and f["rank"] != int(rank)):
         return
+    _fire(f, f"rank {rank} at generation {generation}")
+
+
+def maybe_inject_evaluation(saved: int, rank: int = 0, spec: Optional[str] = None) -> None:
+    """Evaluation recovery tests: fire once ``saved`` results (already pickled) reach ``evaluated=N``."""
+    f = parse(os.environ.get(ENV) if spec is None else spec)
+    if f is None or f["evaluated"] is None or int(saved) < f["evaluated"] or \
+            (f["rank"] is not None and f["rank"] != int(rank)):
+        return
+    _fire(f, f"rank {rank} after {saved} saved evaluations")
+
+
+def _fire(f: dict, what: str) -> None:
     if f["mode"] == "exit":
         os._exit(EXIT_STATUS)
     if f["mode"] == "hang":
         while True:                    # a stalled rank: only the watchdog ends this
             time.sleep(1.0)
-    raise InjectedFault(f"injected fault: rank {rank} at generation {generation}")
+    raise InjectedFault(f"injected fault: {what}")
 
 
 JOB_ORGANISMS = 112      # organisms per pool job in the reference split (logic/experiment.py:170-178)

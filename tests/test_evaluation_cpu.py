@@ -87,6 +87,39 @@ def test_evaluator_and_driver_resume(experiment, tmp_path):
     assert set(flat["serann_id"]) == set(ids)
 
 
+def test_evaluation_dies_midway_and_resumes_from_pickle(experiment, tmp_path, monkeypatch):
+    """An injected death after the first pickle (SERANN_FAULT_INJECT evaluated=2): the relaunch reads the
+    pickle, evaluates only what is missing, and ends with the same results as an uninterrupted run."""
+    from serann.utils.faults import InjectedFault
+    df, data, codec, p, _ = experiment
+    ep = {k: p[k] for k in ("genotype_size", "error_correction_probability", "classification_image_dimensions",
+                            "num_classification_classes", "training_epochs", "training_batch_size")}
+
+    def worker():
+        return SerannEvaluationWorker(ep, data, codec, num_evaluations=2, replications_per_evaluation=4,
+                                      engine="torch", device="cpu", train_cfg=TrainConfig(epochs=1, batch_size=200))
+    ids = list(df.index[:6])
+    quiet = lambda *a, **k: None  # noqa: E731
+    full = SampleDeepEvaluator(df, str(tmp_path / "full.pkl"), ids, worker(), batch=2, log=quiet).run()
+    out = tmp_path / "cut.pkl"
+    monkeypatch.setenv("SERANN_FAULT_INJECT", "evaluated=2,mode=raise")
+    with pytest.raises(InjectedFault):
+        SampleDeepEvaluator(df, str(out), ids, worker(), batch=2, log=quiet, save_every=2).run()
+    monkeypatch.delenv("SERANN_FAULT_INJECT")
+    with open(out, "rb") as f:
+        saved = pickle.load(f)
+    assert sum(1 for v in saved.values() if len(v)) == 2
+    w = worker()
+    calls = []
+    orig = w.run_many
+    w.run_many = lambda rows: calls.append(len(rows)) or orig(rows)
+    res = SampleDeepEvaluator(df, str(out), ids, w, batch=2, log=quiet, save_every=2).run()
+    assert sum(calls) == 4                      # only the missing four were evaluated
+    assert res.keys() == full.keys()
+    for i in ids:
+        assert res[i]["classification_accuracy"] == full[i]["classification_accuracy"], i
+
+
 def test_muller_plot_data(experiment):
     df, *_ = experiment
     pops, adj = prepare_muller_plot_data(df, frequency_threshold=0.0)
