@@ -12,6 +12,8 @@
 #   pop50                   BASELINE config #2: pop 50, example.json, 1 GPU
 #   evaluation              seconds per evaluated genotype
 #   pop50long               BASELINE config #2 at its real length: run_experiment CLI, example.json, 100 generations
+#   tl                      single-stream kernel traces of both fixed populations (scripts/launch_roofline.py)
+#   step                    step wall time on both fixed populations (4 and 1 streams)
 #   evalgeneral             BASELINE config #5: run_evaluation CLI (E = 5, R = 100, general sampler) over ~300
 #                           genotypes of the pop50long experiment; dies after its first 100 pickled results
 #                           (fault injection, exit 75) and is relaunched, resuming from the pickle
@@ -28,7 +30,7 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step $name failed (rc=$rc), stopping"; exit $rc; fi
   # a failing test run (rc 1) may hide a GPU fault caught as an exception: nothing more runs on the GPU then
   if grep -qE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "gpurun_out/$name.log"; then
-    echo "step $name hit a GPU fault, stopping" | tee -a gpurun_out/session.log; exit 3
+    echo "step $name hit a GPU fault, stopping" | tee -a gpurun_out/session.log; exit 98
   fi
   return 0
 }
@@ -41,6 +43,12 @@ STEPS=${STEPS:-tests,bench1}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 has tests && run gputests 1000 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
 has probe && run probe 60 ./scripts/micro/rsrc_probe
+# testsall: the whole suite without -x (the conftest ends the session at a GPU fault), to see every failure
+has testsall && run gputestsall 1000 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
+if has diag96; then
+  run diag_fused 500 python -u scripts/diag_bf16_ratio.py
+  run diag_nogchain 500 env SERANN_FUSE_GCHAIN=0 python -u scripts/diag_bf16_ratio.py gchain_f64_bn_dense gchain_nobn_k9_f100 gchain_relu_conv_fanout gchain_sigmoid_stride2 convpool_bench_a
+fi
 has diag && run diag 600 python -u scripts/diag_grad_err.py
 if has bench2; then
   run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
@@ -64,6 +72,25 @@ has calib && run calib 900 python scripts/calibrate_cost.py --population-file po
 has bench1 && run bench_a 600 python bench.py --steps ${BSTEPS:-3} --warmup 1
 has pop50 && run pop50 600 python bench.py --gpus 1 --pop-per-gpu 50 --parameters serann/parameters/experiment/example.json --steps ${BSTEPS:-3} --warmup 1
 has evaluation && run evaluation 500 python scripts/bench_evaluation.py --genotypes 4 --per-engine 2
+
+# tl: kernel traces of the captured single-stream training step on the two fixed populations, for
+# scripts/launch_roofline.py (per-launch measured vs ideal time)
+if has tl; then
+  mkdir -p gpurun_out/tl
+  for pop in bench_gen3_pop125 ancestor_pop125; do
+    rm -rf gpurun_out/tl/trace
+    run tl_$pop 300 rocprofv3 --kernel-trace -d $R/gpurun_out/tl/trace -o run --output-format csv -- python3 \
+        scripts/bench_step.py --population-file populations/$pop.json --streams 1 --epochs 1
+    f=$(find gpurun_out/tl/trace -name "*kernel_trace.csv" | head -1); cp "$f" gpurun_out/tl/${pop}_s1.csv
+    rm -rf gpurun_out/tl/trace
+  done
+fi
+# step: wall time per step (4 streams and 1) on both fixed populations
+if has step; then
+  for pop in bench_gen3_pop125 ancestor_pop125; do
+    run step_$pop 300 python3 scripts/bench_step.py --population-file populations/$pop.json --streams 4,1 --epochs 2
+  done
+fi
 
 export SERANN_EXPERIMENT_RESULTS_DIR=$R/gpurun_out/ev/exp
 export SERANN_SERANN_EVALUATIONS_DIR=$R/gpurun_out/ev/evals

@@ -28,3 +28,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+_GPU_FAULT_SIGNS = ("illegal memory access", "Memory access fault", "hipErrorIllegalAddress", "HSA_STATUS_ERROR")
+
+
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_makereport(item, call):
+    """A GPU fault poisons the HIP context for every later test: end the session at the first one (even
+    without -x), so nothing else runs on a faulted device."""
+    outcome = yield
+    rep = outcome.get_result()
+    if rep.failed and call.excinfo is not None and any(s in str(call.excinfo.value) for s in _GPU_FAULT_SIGNS):
+        pytest.exit(f"GPU fault in {item.nodeid}: stopping the session", returncode=98)
