@@ -2104,6 +2104,8 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 4, 2>), grid, b2, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError()); return; }
         W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
+        // whole-F tiles of single-split Dense WGRADs (hip_ops.WGRAD_WIDE): X read once per column tile
+        W3(96, 64) W3(128, 64) W3(160, 64) W3(192, 64)
 #undef W3
         throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
     }

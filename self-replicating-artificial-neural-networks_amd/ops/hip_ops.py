@@ -658,6 +658,11 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
+            if mode == MODE_WGRAD and WGRAD_WIDE and 64 < M <= 192 and N > 16 and v < 1000000 \
+                    and -(-K // BK) <= WGRAD_WIDE_MAXK:
+                # one f tile over the whole layer: the X panel of a column tile is read once, not once per
+                # 64-row f tile (a function of the problem alone: its single split is kept)
+                v = next(b for b in (96, 128, 160, 192) if M <= b) * 1000 + 64
             if mode == MODE_WGRAD:
                 bm_, bn_ = gemm3_block(mode, v)
                 if wgrad_row_groups(M, N, K, bm_, bn_) == 2:
@@ -813,6 +818,10 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64, rg: int
 
 
 _WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+# whole-F WGRAD tiles (BMF 96..192 x 64 columns) for Dense problems with F in (64, 192] and a short reduction
+# (<= WGRAD_WIDE_MAXK 32-row k steps: the batch-750 Dense layers, single split -> plain store / fused Adam)
+WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0") != "0"
+WGRAD_WIDE_MAXK = int(_os.environ.get("SERANN_WGRAD_WIDE_MAXK", "64"))
 # m-split WGRAD problems run two row groups of 4 waves per block (gemm3.hip, variant + 500): a block walks
 # 2 x 128 k-steps, so an m-split costs one fixed-point flush per 256 k-steps at the same parallelism
 WGRAD_ROW_GROUPS = int(_os.environ.get("SERANN_WGRAD_ROW_GROUPS", "2"))

@@ -481,3 +481,28 @@ def test_ew_map_reduce_permute():
     n = H.operand((4, 9, 5, 3), torch.bfloat16, DEV)
     _ew_run([H.ew_map_row(n.data_ptr(), (4, 9, 5, 3), x.data_ptr(), (4, 9, 5, 3), ca=-1.0)])
     assert torch.equal(n, -x)
+
+
+@pytest.mark.parametrize("F,N", [(146, 300), (95, 1504), (190, 77), (118, 64)])
+def test_wide_f_dense_wgrad(F, N, monkeypatch):
+    """Whole-F WGRAD tiles (hip_ops.WGRAD_WIDE: BMF 96..192 x 64) on batch-750 Dense problems: Q32 gradient
+    and bias gradient against fp32, single split (plain store), bitwise repeatable."""
+    monkeypatch.setattr(H, "WGRAD_WIDE", True)
+    M = 750
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = H.padded(torch.randn(M, N, device=DEV, generator=g).bfloat16())
+    dz = H.padded(torch.randn(M, F, device=DEV, generator=g).bfloat16())
+    geo = dict(H=1, W=1, C=N, OH=1, OW=1, F=F, KH=1, KW=1, SH=1, SW=1)
+    row = dict(a=dz.data_ptr(), b=x.data_ptr(), M=F, N=N, K=M, flags=H.GF_VEC_A if F % 8 == 0 else 0, **geo)
+    plans = H.gemm3_plan(H.MODE_WGRAD, [dict(row)], [(F, N, M)])
+    assert plans[0][0] % 1000000 // 1000 >= 96, plans[0][0]
+    res = []
+    for _ in range(2):
+        dw = H.operand((F, N), torch.int64, DEV)
+        db = H.operand(F, torch.int64, DEV)
+        _run_gemm(H.MODE_WGRAD, [dict(row, out=dw.data_ptr(), bias=db.data_ptr())], [(F, N, M)])
+        res.append((dw.clone(), db.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    ref = dz.float().t() @ x.float()
+    assert _rel(_q(res[0][0]), ref) < 2e-5
+    assert _rel(_q(res[0][1]), dz.float().sum(0)) < 1e-5
