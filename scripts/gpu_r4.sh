@@ -92,7 +92,9 @@ if has step; then
   done
 fi
 
-export SERANN_EXPERIMENT_RESULTS_DIR=$R/gpurun_out/ev/exp
+# EXPDIR: an experiment results directory shipped with the tree (gpurun_out/ is not pushed), e.g. the
+# pop50long DB copied back for a later evalgeneral call
+export SERANN_EXPERIMENT_RESULTS_DIR=${EXPDIR:-$R/gpurun_out/ev/exp}
 export SERANN_SERANN_EVALUATIONS_DIR=$R/gpurun_out/ev/evals
 if has pop50long; then
   mkdir -p gpurun_out/ev/exp
@@ -100,7 +102,7 @@ if has pop50long; then
       --perf-log gpurun_out/ev/pop50_100gen.jsonl
 fi
 if has evalgeneral; then
-  db=$(ls gpurun_out/ev/exp/*.sqlite | head -1)
+  db=$(ls $SERANN_EXPERIMENT_RESULTS_DIR/*.sqlite | head -1)
   eid=$(basename "$db" .sqlite)
   python - "$eid" <<'PY'
 import json, sys

@@ -284,6 +284,9 @@ __global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restri
     const G3 g = geo3(d);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
+    auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
+    const int kfa = kswz(r16, lane >> 4);
     const int m_w = td.y * BMB + (KW ? 0 : wave * WROWS);
     const int n0 = td.z * BNB;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
@@ -874,6 +877,9 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     const Div dCp = mkdiv(d.dvCp);
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
+    auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
+    const int kfa = kswz(r16, lane >> 4);
     const int ohw = g.OH * g.OW;
     const int b = td.y, m0 = td.z, n0 = td.w * BN;
     const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
@@ -1775,8 +1781,12 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
 // operand tiles go through LDS, so the weight tile is fetched once per block instead of once per
 // wave (the direct-fragment kernel re-reads B in every wave), and the next k-step's global loads are in
 // flight while the current step multiplies (register-staged double buffer, one barrier per step).
-// Rows of 40 elements (80 B, an odd number of 16-B slots) keep the 16-row ds_read_b128 fragment reads
-// conflict-free.  The epilogue stages the block's tile in LDS and streams it out with 16-B stores
+// LDS rows are 32 elements (64 B) with the four 16-B k chunks of a row XOR-swizzled by its row quad
+// (row >> 2) & 3 -> {0, 2, 3, 1}: every 16-lane group of a ds_read_b128 fragment read ({0-3, 12-15,
+// 20-27}, ...: rows 0-3 and 12-15 at one k chunk, rows 4-11 at the next) then hits 16 distinct 16-B slots of
+// the 256-B bank row, and the 8-lane groups of the ds_write_b128 staging stores stay inside one 128-B
+// window.  (The former 80-B padded rows put rows 1 and 4 + chunk 1 on one slot: 5.3 conflict cycles per LDS
+// instruction measured, profiles/r4/pmc_heavy_launches.txt.)  The epilogue stages the block's tile in LDS and streams it out with 16-B stores
 // when the block spans all N columns (the usual case: N <= 128).
 // BT (DGRAD only): B is the layer's weight matrix in its natural [K = F][N = C] layout (row stride ldb,
 // default N) instead of the transposed copy Wt[C][F]: a k-step's B tile is loaded as 32 k rows x BN
@@ -1786,7 +1796,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
 template <int MODE, int BN, bool BT = false>
 __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restrict__ descs,
                                                        const int4* __restrict__ tiles) {
-    constexpr int BM = 128, BK = 32, LDS_ROW = BK + 8;
+    constexpr int BM = 128, BK = 32, LDS_ROW = BK;
     constexpr int NTW = BN / 32;                     // 16-col tiles per wave (2 waves along n)
     constexpr int LDBT = BN + 8;                     // BT: k-major B row (multiple of 8 elements)
     constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = BT ? 2 * BK * LDBT : 2 * BN * LDS_ROW;
@@ -1803,7 +1813,10 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const int lda = (MODE == MODE_FWD) ? (int)d.C : K;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    const int r16 = lane & 15;
+    // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
+    auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
+    const int kfa = kswz(r16, lane >> 4);
     const int m0 = td.y * BM, n0 = td.z * BN;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
     const int64_t a_elems = (int64_t)M * lda;
@@ -1817,6 +1830,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 
     // loaders: thread t -> (row t/4 + 64 i, k chunk (t % 4) * 8)
     const int lr = t >> 2, lk = (t & 3) * 8;
+    const int lks = kswz(lr, t & 3);                 // (rows lr + 64 i share lr's row quad)
     constexpr int BPT = (BN + 63) / 64;              // B chunks per thread (BN = 160 / 192: the last partial)
     // BT loader: thread t -> (k row t / NCH + BKP i, n chunk (t % NCH) * 8)
     constexpr int NCH = BN / 8, BKP = 256 / NCH, BTP = (BK + BKP - 1) / BKP;
@@ -1866,7 +1880,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             uint4 v = ra[i];
             if (gact != ACT_LINEAR) v = mul_act_grad(v, ry[i], gact);
             if (arun < 8) v = splice(v, zero, arun);
-            *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lk]) = v;
+            *reinterpret_cast<uint4*>(&As[(buf * BM + lr + 64 * i) * LDS_ROW + lks]) = v;
         }
         if (BT) {
 #pragma unroll
@@ -1876,7 +1890,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         } else {
 #pragma unroll
             for (int i = 0; i < BPT; ++i)
-                if (lr + 64 * i < BN) *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lk]) = rb[i];
+                if (lr + 64 * i < BN) *reinterpret_cast<uint4*>(&Bs[(buf * BN + lr + 64 * i) * LDS_ROW + lks]) = rb[i];
         }
     };
 
@@ -1897,7 +1911,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         Frag fa[4], fb[NTW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            fa[i].u = *reinterpret_cast<const uint4*>(&As[(buf * BM + wr * 64 + i * 16 + r16) * LDS_ROW + kg]);
+            fa[i].u = *reinterpret_cast<const uint4*>(&As[(buf * BM + wr * 64 + i * 16 + r16) * LDS_ROW + kfa]);
         if (BT) {
             const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
@@ -1908,7 +1922,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         } else {
 #pragma unroll
             for (int j = 0; j < NTW; ++j)
-                fb[j].u = *reinterpret_cast<const uint4*>(&Bs[(buf * BN + wc * (BN / 2) + j * 16 + r16) * LDS_ROW + kg]);
+                fb[j].u = *reinterpret_cast<const uint4*>(&Bs[(buf * BN + wc * (BN / 2) + j * 16 + r16) * LDS_ROW + kfa]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
