@@ -23,9 +23,10 @@ R=$(pwd)
 run() {
   local name=$1; shift; local to=$1; shift
   echo "=== $name ===" | tee -a gpurun_out/session.log
+  local t0=$(date +%s%N)
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "rc=$rc" | tee -a gpurun_out/session.log
+  echo "rc=$rc wall_ms=$(( ($(date +%s%N) - t0) / 1000000 ))" | tee -a gpurun_out/session.log
   tail -4 "gpurun_out/$name.log" | cut -c1-600 | tee -a gpurun_out/session.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step $name failed (rc=$rc), stopping"; exit $rc; fi
   # a failing test run (rc 1) may hide a GPU fault caught as an exception: nothing more runs on the GPU then
@@ -107,14 +108,15 @@ if has evalgeneral; then
   python - "$eid" <<'PY'
 import json, sys
 p = json.load(open("serann/parameters/evaluation/general.json"))
-p.update(experiment_id=sys.argv[1], generation_step=1, samples_per_generation=3)
+p.update(experiment_id=sys.argv[1], generation_step=1, samples_per_generation=2)
 json.dump(p, open("gpurun_out/ev/general_r4.json", "w"), indent=1)
 PY
   echo "=== evalgeneral_cut ===" | tee -a gpurun_out/session.log
+  t0=$(date +%s%N)
   SERANN_FAULT_INJECT=evaluated=100,mode=exit timeout -k 10 900 python -u serann_evaluation/run_evaluation.py \
       -p gpurun_out/ev/general_r4.json -n general_r4 > gpurun_out/evalgeneral_cut.log 2>&1
   rc=$?
-  echo "rc=$rc (75 = the injected death after the first pickle)" | tee -a gpurun_out/session.log
+  echo "rc=$rc wall_ms=$(( ($(date +%s%N) - t0) / 1000000 )) (75 = the injected death after the first pickle)" | tee -a gpurun_out/session.log
   if [ $rc -ne 75 ] && [ $rc -ne 0 ]; then echo "evalgeneral_cut failed (rc=$rc), stopping"; exit $rc; fi
   run evalgeneral 900 python -u serann_evaluation/run_evaluation.py -p gpurun_out/ev/general_r4.json -n general_r4
 fi

@@ -160,6 +160,27 @@ __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_p, const bf16_t* hi
     return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// XOR swizzle of an unpadded m-major LDS tile with NB 32-B blocks (16 bf16) per row, read by tr_frag
+// (ds_read_b64_tr_b16: two 32-lane groups, each 8 rows {0-3, 8-11} (+4, + 32 per sub-step) x 32 B of one
+// column block).  Block L = row * NB + col / 16 moves inside its aligned 256-B group (8 blocks) by a
+// function of the group index only (a bijection): the 8 rows of a read group land on the 8 distinct
+// 32-B bank blocks of the 256-B bank row, and the 16-B staging stores of 8 consecutive lanes (an aligned
+// quad of blocks) keep distinct 128-B bank windows.  Per-NB masks from an exhaustive search over linear
+// maps of the group bits (padding rows to 72 / 136 elements, as before, left 2-way conflicts).
+template <int NB>
+__device__ __forceinline__ int tr_swz(int row, int col) {
+    const int L = row * NB + (col >> 4), G = L >> 3;
+    int h;
+    if constexpr (NB == 1) h = (G & 1) << 2;
+    else if constexpr (NB == 2 || NB == 6 || NB == 10) h = (G >> 1) & 1;
+    else if constexpr (NB == 4 || NB == 12) h = (G & 1) | ((G >> 1) & 2);
+    else if constexpr (NB == 8) h = (G & 3) | ((G >> 1) & 4);
+    else h = ((G >> 1) & 3) | ((G >> 2) & 4);
+    static_assert(NB == 1 || NB == 2 || NB == 4 || NB == 6 || NB == 8 || NB == 10 || NB == 12 || NB == 16,
+                  "tr_swz: no conflict-free map searched for this row width");
+    return ((L ^ h) << 4) | (col & 15);
+}
+
 // ---- im2col chunk (FWD A operand, WGRAD B operand) -------------------------------------------
 // Per-lane decomposition of the reduction chunk starting at k = (kh, kw, c).
 struct KChunk {
@@ -515,7 +536,8 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
                                                             const int4* __restrict__ tiles) {
     constexpr int BKM = 64;
     constexpr int NTH = 64 * NWV;                    // threads per row group (RG row groups per block)
-    constexpr int LDA = BMF + 8, LDB = BNK + 8;
+    constexpr int LDA = BMF, LDB = BNK;              // unpadded rows, XOR-swizzled blocks (tr_swz)
+    constexpr int NBA = BMF / 16, NBB = BNK / 16;
     constexpr int SMEM = RG * BKM * (LDA + LDB);     // bf16 elements: one As / Bs pair per row group
     __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
     const int rg = threadIdx.x / NTH;
@@ -641,11 +663,11 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
             if (a_nv < 8) v = splice(v, make_uint4(0, 0, 0, 0), a_nv);
             ra[p].u = v;                                 // (bias_acc reads dZ)
             const int r = a_r + p * AROWS;
-            if (a_act && r < BKM) *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = v;
+            if (a_act && r < BKM) *reinterpret_cast<uint4*>(&As[tr_swz<NBA>(r, a_f)]) = v;
         }
 #pragma unroll
         for (int p = 0; p < BPASS; ++p)
-            if (b_r + p * BROWS < BKM) *reinterpret_cast<uint4*>(&Bs[(b_r + p * BROWS) * LDB + b_k]) = rbv[p].u;
+            if (b_r + p * BROWS < BKM) *reinterpret_cast<uint4*>(&Bs[tr_swz<NBB>(b_r + p * BROWS, b_k)]) = rbv[p].u;
     };
 
     f32x4_t acc[TF][TK];
@@ -668,12 +690,12 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
 #pragma unroll
             for (int i = 0; i < TF; ++i) {
                 const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
-                fa[i] = tr_frag(&As[mr * LDA + col], &As[(mr + 4) * LDA + col]);
+                fa[i] = tr_frag(&As[tr_swz<NBA>(mr, col)], &As[tr_swz<NBA>(mr + 4, col)]);
             }
 #pragma unroll
             for (int j = 0; j < TK; ++j) {
                 const int col = wk * (BNK / WC) + j * 16 + 4 * pp;
-                fbk[j] = tr_frag(&Bs[mr * LDB + col], &Bs[(mr + 4) * LDB + col]);
+                fbk[j] = tr_frag(&Bs[tr_swz<NBB>(mr, col)], &Bs[tr_swz<NBB>(mr + 4, col)]);
             }
 #pragma unroll
             for (int i = 0; i < TF; ++i)
@@ -1047,7 +1069,7 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 template <int BMF, int BNK, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
-    constexpr int TM = 128, LDA = BMF + 8;
+    constexpr int TM = 128, LDA = BMF, NBA = BMF / 16;   // dZ tile: unpadded rows, tr_swz blocks
     // patch + one 16-B dump slot for the staging writes of pieces past the chunk's patch
     __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH + 8];
     __shared__ __attribute__((aligned(16))) bf16_t As[TM * LDA];
@@ -1198,7 +1220,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
                 uint4 v = apre[k];
                 if (g.act != ACT_LINEAR) v = mul_act_grad(v, ypre[k], g.act);
                 if (a_nv < 8) v = splice(v, zero, a_nv);
-                *reinterpret_cast<uint4*>(&As[r * LDA + a_f]) = v;
+                *reinterpret_cast<uint4*>(&As[tr_swz<NBA>(r, a_f)]) = v;
                 if (do_bias) {
                     Frag fv;
                     fv.u = v;
@@ -1219,7 +1241,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
 #pragma unroll
             for (int i = 0; i < TF; ++i) {
                 const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
-                fa[i] = tr_frag(&As[mr * LDA + col], &As[(mr + 4) * LDA + col]);
+                fa[i] = tr_frag(&As[tr_swz<NBA>(mr, col)], &As[tr_swz<NBA>(mr + 4, col)]);
             }
 #pragma unroll
             for (int j = 0; j < TK; ++j) fbk[j] = tr_frag(p0 + coff[j], p1 + coff[j]);

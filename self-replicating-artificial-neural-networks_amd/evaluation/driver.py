@@ -137,6 +137,7 @@ class SampleDeepEvaluator:
             if remaining else 0
         done = 0
         durations = []
+        t_run = time.perf_counter()
         for k in range(rounds):
             t0 = time.perf_counter()
             chunk = mine[k * self.batch:(k + 1) * self.batch]
@@ -158,7 +159,7 @@ class SampleDeepEvaluator:
             durations.append((time.perf_counter() - t0) / max(1, sum(len(p) for p in gathered)))
             avg = float(np.mean(durations[-200:]))
             self.log(f"{done}/{len(remaining)} jobs done. Average evaluation time: {int(avg) // 60:02d}:"
-                     f"{int(avg) % 60:02d}.")
+                     f"{int(avg) % 60:02d}. ({avg:.3f} s per genotype, {time.perf_counter() - t_run:.1f} s elapsed)")
             se = self.save_every
             if comm.is_root and (done // se != (done - sum(len(p) for p in gathered)) // se or k == rounds - 1):
                 self.log("Saving to disk.")

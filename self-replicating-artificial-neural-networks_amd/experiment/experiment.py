@@ -164,6 +164,9 @@ class Experiment:
                           mean_val_acc=float(np.nanmean(current["classification_validation_accuracy"]))
                           if len(valid_serann) else float("nan"),
                           stats_db_seconds=t_db - t_stats)
+            wp = getattr(self._worker, "last_phases", None)
+            if wp:
+                record["shard_phases"] = {k: round(v, 4) for k, v in wp.items()}      # this rank's shard
             if self._comm.world_size > 1:
                 ms = [v for v in times["rank_measured_s"] if v > 0]
                 record["rank_imbalance"] = max(ms) / (sum(ms) / len(ms)) if ms else float("nan")

@@ -119,13 +119,24 @@ class ShardWorker:
         packed = None            # device tensor (HIP epilogue) or numpy, [n][pool][nbytes]
         times = [0.0, 0.0]
 
+        # host-side phases of the shard (seconds, summed over waves): where a generation's time goes
+        # besides the training loop itself (``learning_time``)
+        ph = self.last_phases = dict.fromkeys(("construct", "plan", "fit", "test_eval", "replicate", "close"), 0.0)
+
         def run_wave(members: List[int], batch: Optional[int]):
             wcfg = cfg if batch is None else dataclasses.replace(cfg, batch_size=int(batch))
+            tc = time.perf_counter()
             engine = make_engine(self.engine_name, [irs[i] for i in members], [seeds[i] for i in members],
                                  self.device, wcfg)
+            ph["construct"] += time.perf_counter() - tc
             try:
+                tc = time.perf_counter()
                 fit = engine.fit(d, wcfg)
+                ph["fit"] += time.perf_counter() - tc
+                ph["plan"] += float(getattr(fit, "extra", None) and fit.extra.get("plan_s", 0.0) or 0.0)
+                tc = time.perf_counter()
                 test_acc = engine.evaluate(d.test_x, d.test_labels, d.test_g, wcfg)
+                ph["test_eval"] += time.perf_counter() - tc
                 outs, rt = None, 0.0
                 if num_replications > 0:
                     t0 = time.perf_counter()
@@ -137,8 +148,11 @@ class ShardWorker:
                         outs = np.packbits(np.stack([replication_bits(o) for o in
                                                      engine.replicate(genotypes[members], images, wcfg)]), axis=-1)
                     rt = time.perf_counter() - t0
+                    ph["replicate"] += rt
             finally:
+                tc = time.perf_counter()
                 engine.close()
+                ph["close"] += time.perf_counter() - tc
             return members, fit, test_acc, outs, fit.learning_time, rt
 
         def on_fail(members: List[int]):

@@ -115,10 +115,13 @@ def test_injected_fault_then_exact_resume(tmp_path, small_data, monkeypatch):
 
 def test_fault_spec_parsing():
     from serann.utils.faults import InjectedFault, maybe_inject, parse
-    assert parse("generation=3,rank=1,mode=exit") == {"generation": 3, "rank": 1, "mode": "exit"}
+    assert parse("generation=3,rank=1,mode=exit") == {"generation": 3, "evaluated": None, "rank": 1, "mode": "exit"}
+    assert parse("evaluated=100,mode=exit") == {"generation": None, "evaluated": 100, "rank": None, "mode": "exit"}
     assert parse("") is None
     with pytest.raises(ValueError):
         parse("rank=1")
+    with pytest.raises(ValueError):
+        parse("generation=1,evaluated=2")                  # exactly one trigger
     maybe_inject(3, rank=0, spec="generation=3,rank=1")     # other rank: no fault
     maybe_inject(2, rank=1, spec="generation=3,rank=1")     # other generation: no fault
     with pytest.raises(InjectedFault):
