@@ -466,10 +466,10 @@ class HipRiboTrainer:
         return out
 
     def state_dict(self):
-        """Both layouts: the flat arenas (exact, fast resume on this engine) and per-parameter lists in
-        ``model.parameters()`` order, so a HIP checkpoint resumes on the torch engine too."""
-        n = self.pa.size
-        return {"t": int(self.step_i.item()), "m_arena": self.m[:n].detach().cpu(), "v_arena": self.v[:n].detach().cpu(),
+        """Per-parameter moment lists in ``model.parameters()`` order (the torch engine's format), so a HIP
+        checkpoint resumes on either engine; the flat arenas are not stored a second time (load_state_dict
+        still reads the arena form of older checkpoints)."""
+        return {"t": int(self.step_i.item()),
                 "m": [v.detach().cpu().contiguous() for v in self._moment_views(self.m)],
                 "v": [v.detach().cpu().contiguous() for v in self._moment_views(self.v)]}
 

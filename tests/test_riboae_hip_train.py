@@ -115,7 +115,7 @@ def test_hip_loss_curve_matches_torch_path(tmp_path):
     assert curves["hip"][-40:].mean() < 0.8 * curves["hip"][:10].mean()       # it learns
     assert abs(a - b) < 0.02 * abs(b), (a, b)
     m2, ck = load_checkpoint(str(tmp_path / "r_hip_b200.pt"))
-    assert ck["step"] == 200 and "m_arena" in ck["optimizer"]
+    assert ck["step"] == 200 and "m" in ck["optimizer"] and "m_arena" not in ck["optimizer"]
 
 
 def test_checkpoint_moments_cross_engines(tmp_path):
