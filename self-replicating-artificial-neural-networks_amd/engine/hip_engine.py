@@ -23,6 +23,7 @@ kernels -- no host-driven torch op anywhere in a plan.
 from __future__ import annotations
 
 import math
+import threading
 import time
 import weakref
 from dataclasses import dataclass, field
@@ -319,6 +320,7 @@ class HipPopulationEngine(PopulationEngine):
         self.plans: Dict[tuple, Plan] = {}
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.timings: Dict[str, float] = {}
+        self._bg = threading.local()                 # fit's background plan builder (_upload_fence)
 
     # ---------------------------------------------------------------------------------------------
     # parameters
@@ -1127,7 +1129,7 @@ class HipPopulationEngine(PopulationEngine):
 
         plan.fwd_count = len(plan.launches)
         if not train:
-            torch.cuda.synchronize(self.device)      # upload fence, as at the end of the train plan
+            self._upload_fence()                     # as at the end of the train plan
             return plan
 
         # ---- backward --------------------------------------------------------------------------
@@ -1430,12 +1432,21 @@ class HipPopulationEngine(PopulationEngine):
                 for r in wg_rows:
                     r["adam"] = adam_ctx
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
-        # descriptor / tile tables are uploaded from pageable host memory: fence them (and any
-        # outstanding work on other streams) before a launch can read them.  Plans are built once per
-        # generation, so this costs nothing on the training hot path.
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+        # descriptor / tile tables are uploaded from pageable host memory: fence them before a launch can
+        # read them.  Plans are built once per generation, so this costs nothing on the training hot path.
+        self._upload_fence()
         return plan
+
+    def _upload_fence(self):
+        """Device-wide synchronize (uploads and any outstanding work on other streams) -- or, for a plan
+        built by fit's background thread while the captured training graph runs, only the building thread's
+        upload stream."""
+        if self.device.type != "cuda":
+            return
+        if getattr(self._bg, "stream_only", False):
+            torch.cuda.current_stream(self.device).synchronize()
+        else:
+            torch.cuda.synchronize(self.device)
 
     # ---------------------------------------------------------------------------------------------
     # execution
@@ -1467,6 +1478,7 @@ class HipPopulationEngine(PopulationEngine):
 
         t_plan = time.perf_counter()
         mem = self._alloc_buffers(B, with_grads=True)
+        self.timings["alloc_s"] = time.perf_counter() - t_plan
         self._train_mem = mem
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(P)]
         targets = [gb.data_ptr()] * P
@@ -1510,15 +1522,48 @@ class HipPopulationEngine(PopulationEngine):
         # its own activation buffers; it reads the first Br rows of the shared batch buffers.
         full_steps = split // B
         Br = split - full_steps * B
-        rem_plans, rem_ws = None, None
-        if Br > 0 and steps > full_steps:
-            mem_r = self._alloc_buffers(Br, with_grads=True)
-            self._train_mem_rem = mem_r
-            rem_plans = [self._build_plan("train", Br, mem_r, inputs, yb.data_ptr(), targets, metrics, orgs=g_,
-                                          adam_ctx=actx_ptr) for g_ in groups]
-            rem_ws = mem_r["ws"].t
-        skip_rem = skip_mask(rem_plans) if rem_plans is not None else None
-        self._adam_skip = (skip_main, skip_rem)          # referenced by the captured graph
+        rem = {"plans": None, "ws": None, "skip": None}
+
+        def build_rest():
+            """The remainder step's plans (and the validation plan): built while the captured graph runs
+            the first epoch's full steps when possible (:func:`start_rest`), else before training."""
+            if Br > 0 and steps > full_steps:
+                mem_r = self._alloc_buffers(Br, with_grads=True)
+                self._train_mem_rem = mem_r
+                rem["plans"] = [self._build_plan("train", Br, mem_r, inputs, yb.data_ptr(), targets, metrics,
+                                                 orgs=g_, adam_ctx=actx_ptr) for g_ in groups]
+                rem["ws"] = mem_r["ws"].t
+                rem["skip"] = skip_mask(rem["plans"])
+            self._infer_plan(B)
+        bg = {"thread": None, "err": None, "stream": None}
+
+        def start_rest():
+            if dev.type != "cuda":
+                build_rest()
+                return
+            side = bg["stream"] = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream())
+
+            def work():
+                self._bg.stream_only = True
+                try:
+                    with torch.cuda.stream(side):
+                        build_rest()
+                except BaseException as e:        # re-raised by join_rest on the fitting thread
+                    bg["err"] = e
+                finally:
+                    self._bg.stream_only = False
+            bg["thread"] = threading.Thread(target=work, name="serann-plan-build", daemon=True)
+            bg["thread"].start()
+
+        def join_rest():
+            if bg["thread"] is not None:
+                bg["thread"].join()
+                bg["thread"] = None
+                if bg["err"] is not None:
+                    raise bg["err"]
+                torch.cuda.current_stream().wait_stream(bg["stream"])
+            self._adam_skip = (skip_main, rem["skip"])       # referenced by the captured graph
 
         def step(pls=plans, nb=B, wsb=ws, base=0, ctr=True, skip=skip_main):
             s = H.stream_handle()
@@ -1546,10 +1591,13 @@ class HipPopulationEngine(PopulationEngine):
             L.counter_add(counter.data_ptr(), 1, s)
 
         def remainder_step():
-            step(rem_plans, Br, rem_ws, full_steps * B, False, skip_rem)
+            step(rem["plans"], Br, rem["ws"], full_steps * B, False, rem["skip"])
 
         use_graph = full_steps > 1
         graph = None
+        if not (use_graph and cfg.epochs > 0 and min(steps, full_steps) > 1):
+            build_rest()                        # no captured graph to overlap with
+            join_rest()
         self.timings["plan_s"] = time.perf_counter() - t_plan
         self.timings["launches_per_step"] = sum(len(pl.launches) for pl in plans) + 5
         self.timings["stream_groups"] = len(plans)
@@ -1577,6 +1625,7 @@ class HipPopulationEngine(PopulationEngine):
                         step()
                 torch.cuda.current_stream().wait_stream(s_)
                 remaining = nfull - 1
+                start_rest()                    # CPU-side plan building overlaps the replays below
             else:
                 remaining = nfull
             ev = None
@@ -1594,7 +1643,8 @@ class HipPopulationEngine(PopulationEngine):
                 ev[1].record()
                 ev[1].synchronize()
                 self.timings["replay_ms_per_step"] = ev[0].elapsed_time(ev[1]) / remaining
-            if rem_plans is not None and steps > nfull:
+            join_rest()
+            if rem["plans"] is not None and steps > nfull:
                 remainder_step()
                 total += 1
             m = H.from_q32(metrics)
@@ -1605,9 +1655,10 @@ class HipPopulationEngine(PopulationEngine):
         self._train_mem = mem
         self.graph = graph
         # every buffer the captured graph addresses lives as long as the graph does
-        self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem_plans)
+        self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem["plans"])
         return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
-                         extra={"plan_s": self.timings["plan_s"], "launches_per_step": self.timings["launches_per_step"]})
+                         extra={"plan_s": self.timings["plan_s"], "alloc_s": self.timings["alloc_s"],
+                                "launches_per_step": self.timings["launches_per_step"]})
 
     # ---------------------------------------------------------------------------------------------
     def export_arena(self, i: int, arena: torch.Tensor) -> Dict[int, Dict[str, np.ndarray]]:

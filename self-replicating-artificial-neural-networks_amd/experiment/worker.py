@@ -121,7 +121,8 @@ class ShardWorker:
 
         # host-side phases of the shard (seconds, summed over waves): where a generation's time goes
         # besides the training loop itself (``learning_time``)
-        ph = self.last_phases = dict.fromkeys(("construct", "plan", "fit", "test_eval", "replicate", "close"), 0.0)
+        ph = self.last_phases = dict.fromkeys(("construct", "alloc", "plan", "fit", "test_eval", "replicate", "close"),
+                                              0.0)
 
         def run_wave(members: List[int], batch: Optional[int]):
             wcfg = cfg if batch is None else dataclasses.replace(cfg, batch_size=int(batch))
@@ -133,7 +134,9 @@ class ShardWorker:
                 tc = time.perf_counter()
                 fit = engine.fit(d, wcfg)
                 ph["fit"] += time.perf_counter() - tc
-                ph["plan"] += float(getattr(fit, "extra", None) and fit.extra.get("plan_s", 0.0) or 0.0)
+                ex = getattr(fit, "extra", None) or {}
+                ph["plan"] += float(ex.get("plan_s", 0.0))          # includes the buffer allocation
+                ph["alloc"] += float(ex.get("alloc_s", 0.0))
                 tc = time.perf_counter()
                 test_acc = engine.evaluate(d.test_x, d.test_labels, d.test_g, wcfg)
                 ph["test_eval"] += time.perf_counter() - tc
