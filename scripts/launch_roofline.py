@@ -51,7 +51,9 @@ def gemm_cost(mode, r):
         rows = M // max(1, int(r["H"]) * int(r["W"]))         # batch
         dz = rows * int(r["OH"]) * int(r["OW"]) * int(r["F"]) * 2
         y = dz if int(r["act"]) else 0
-        return dz + y + N * K * 2 + M * N * 2, fl
+        # GF_NBNSUM: no dY store, fp32 per-column BN sums per 128-row m tile instead
+        out = -(-M // 128) * N * H.NBN_NSUM * 4 if flags & H.GF_NBNSUM else M * N * 2
+        return dz + y + N * K * 2 + out, fl
     # WGRAD: M = F, N = KH KW C, K = rows
     rows = K // max(1, int(r["OH"]) * int(r["OW"]))
     dz = K * int(r["F"]) * 2
@@ -103,6 +105,9 @@ def launch_cost(la, B):
             b += img + pooled
             f += 2.0 * int(r["B"]) * int(r["OH"]) * int(r["OW"]) * int(r["F"]) * int(r["KH"]) * int(r["KW"])
         return b, f
+    if k == "nbn" and la.arg[0] == 6:
+        rows = _rows(la, H.NBN_DTYPE)                          # phase 6: read the DGRAD's partial sums
+        return float(sum(int(r["mtiles"]) * int(r["np"]) * int(r["F"]) * H.NBN_NSUM * 4 for r in rows)), 0.0
     if k == "nbn":
         rows = _rows(la, H.NBN_DTYPE)
         b = f = 0.0

@@ -1815,7 +1815,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
 // columns (16-B chunks along n), staged k-major in LDS ([32][BN + 8]) and its MFMA fragments are read
 // with ds_read_b64_tr_b16 (lane i of a 16-lane group receives column i of 4 consecutive k rows, k row q
 // in element q -- the k order of the ds_read_b128 A fragments).  No per-step weight transpose launch.
-template <int MODE, int BN, bool BT = false>
+template <int MODE, int BN, bool BT = false, bool NS = false>
 __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restrict__ descs,
                                                        const int4* __restrict__ tiles) {
     constexpr int BM = 128, BK = 32, LDS_ROW = BK;
@@ -1823,7 +1823,10 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     constexpr int LDBT = BN + 8;                     // BT: k-major B row (multiple of 8 elements)
     constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = BT ? 2 * BK * LDBT : 2 * BN * LDS_ROW;
     constexpr int STAGE = BM * (BN + 8);             // epilogue staging (bf16 elements, padded rows)
-    constexpr int LDSN = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
+    constexpr int LDSN0 = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
+    // NS epilogue staging (floats): x tile [BM][BN / 8 + 2], dY slice [BM][33], wave sums [4][32][8]
+    constexpr int NSLDS = NS ? 2 * (BM * (BN / 8 + 2) + BM * 33 + 4 * 32 * 8) : 0;
+    constexpr int LDSN = LDSN0 > NSLDS ? LDSN0 : NSLDS;
     __shared__ __attribute__((aligned(16))) bf16_t lds[LDSN];
     bf16_t* As = lds;                                // [2][BM][LDS_ROW]
     bf16_t* Bs = lds + ABYTES;                       // [2][BN][LDS_ROW]
@@ -1959,6 +1962,99 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const float* bias = (MODE == MODE_FWD) ? reinterpret_cast<const float*>(d.bias) : nullptr;
     const int oact = (MODE == MODE_FWD) ? act : ACT_LINEAR;
     const int rq = (lane >> 4) * 4;
+    if constexpr (MODE == MODE_DGRAD && NS) {
+        // NS (GF_NBNSUM; its own instantiation, so the other DGRADs keep their registers / occupancy).
+        // This DGRAD produces dY of a fused raw-input Dense -> BatchNormalization pair with ONE input channel
+        // (nbn.hip; the planner's condition) and is its only producer: dY is never stored.  Per column n
+        // (BN row r = m * np + n / F, channel f = n % F) the block reduces, over its rows and from the fp32
+        // accumulators, what the BN backward and the Dense WGRAD need (y recomputed from the raw input x
+        // exactly as nbn.hip does, xhat = (y - mean) invstd, a = act'(y)):
+        //   [0] dy  [1] dy xhat  [2] a dy  [3] a xhat  [4] a  [5] a x dy  [6] a x xhat  [7] a x
+        // and stores them to NbnDesc::part, slot m tile -- plain stores, one writer per (slot, column).  nbn
+        // phase 6 adds the slots in a fixed order and forms dgamma, dbeta, dW, db.
+        constexpr int NSUM = 8;
+        const NbnDesc& nd = *reinterpret_cast<const NbnDesc*>(d.ext);
+        const int Fb = (int)nd.F, ldxr = (int)nd.ldx, NPc = (int)nd.np, nact = (int)nd.act;
+        const bf16_t* __restrict__ Xr = reinterpret_cast<const bf16_t*>(nd.x);
+        const bf16_t* __restrict__ Wn = reinterpret_cast<const bf16_t*>(nd.w);
+        const float* __restrict__ nb = reinterpret_cast<const float*>(nd.bias);
+        const float* __restrict__ nmean = reinterpret_cast<const float*>(nd.mean);
+        const float* __restrict__ nis = reinterpret_cast<const float*>(nd.invstd);
+        // the block's raw inputs x[m][p] (rows m0.., positions p0..p1 of its columns) staged once in LDS, and
+        // per column tile j the fp32 dY slice [BM][32] (both waves along n): the sums are then formed from LDS
+        // by (column, 16-row group) threads -- reading the accumulators in place would keep the whole tile
+        // in VGPRs through the epilogue, and that peak (not the k loop) would set the occupancy
+        constexpr int SLD = 33;                          // slice row stride (floats): conflict-free column reads
+        const int p0 = n0 / Fb, npos = min(N - 1, n0 + BN - 1) / Fb - p0 + 1;
+        float* xs = reinterpret_cast<float*>(lds);       // [BM][npos]; the k loop ended on a barrier
+        float* sl = xs + BM * (BN / 8 + 2);              // [BM][SLD]
+        float* red = sl + BM * SLD;                      // [4 waves][32 columns][NSUM]
+        static_assert((BM * (BN / 8 + 2) + BM * SLD + 4 * 32 * NSUM) * 4 <= LDSN * 2,
+                      "NBNSUM staging must fit in the LDS tiles");
+        for (int u = t; u < BM * npos; u += 256) {
+            const int rl = u / npos, pp = u - rl * npos;
+            const int row = min(m0 + rl, M - 1);
+            xs[u] = bf2f(Xr[((int64_t)row * NPc + p0 + pp) * ldxr]);
+        }
+        float* __restrict__ part = reinterpret_cast<float*>(nd.part) + (int64_t)td.y * N * NSUM;
+        const int sc = t & 31, sg = t >> 5;              // column of the slice, 16-row group
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sl[(wr * 64 + i * 16 + rq + r) * SLD + wc * 16 + r16] = acc[i][j][r];
+            __syncthreads();
+            const int cl = (sc >> 4) * (BN / 2) + j * 16 + (sc & 15);   // block column of slice column sc
+            const int n = n0 + cl;
+            float sm[NSUM];
+#pragma unroll
+            for (int q = 0; q < NSUM; ++q) sm[q] = 0.f;
+            if (n < N) {
+                const int p = n / Fb, f = n - p * Fb;
+                const float w = bf2f(Wn[f]), bv = nb ? nb[f] : 0.f, mu = nmean[f], is = nis[f];
+                const float* xp = xs + (p - p0);
+#pragma unroll 4
+                for (int rr = 0; rr < 16; ++rr) {
+                    const int rl = sg * 16 + rr;
+                    if (m0 + rl >= M) break;
+                    const float xv = xp[rl * npos];
+                    float v = bv;                        // nbn.hip nbn_y: bias first, then the product
+                    v += xv * w;
+                    const float y = apply_act(v, nact);
+                    const float xh = (y - mu) * is;
+                    const float a = nact == ACT_RELU ? (y > 0.f ? 1.f : 0.f)
+                                                     : (nact == ACT_SIGMOID ? y * (1.f - y) : 1.f);
+                    const float gy = sl[rl * SLD + sc];
+                    const float ax = a * xv;
+                    sm[0] += gy;
+                    sm[1] += gy * xh;
+                    sm[2] += a * gy;
+                    sm[3] += a * xh;
+                    sm[4] += a;
+                    sm[5] += ax * gy;
+                    sm[6] += ax * xh;
+                    sm[7] += ax;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NSUM; ++q) sm[q] += __shfl_xor(sm[q], 32, 64);   // the wave's two row groups
+            if (lane < 32) {
+#pragma unroll
+                for (int q = 0; q < NSUM; ++q) red[(wave * 32 + sc) * NSUM + q] = sm[q];
+            }
+            __syncthreads();
+            {
+                const int c2 = t / NSUM, q = t - c2 * NSUM;          // 32 columns x 8 sums = 256 threads
+                const int n2 = n0 + (c2 >> 4) * (BN / 2) + j * 16 + (c2 & 15);
+                if (n2 < N)
+                    part[(int64_t)n2 * NSUM + q] = red[c2 * NSUM + q] + red[(32 + c2) * NSUM + q] +
+                                                   red[(64 + c2) * NSUM + q] + red[(96 + c2) * NSUM + q];
+            }
+            __syncthreads();                             // the slice and red are rewritten by the next tile
+        }
+        return;
+    }
     if (MODE == MODE_FWD && (flags & GF_SPLITWS)) {
         // raw fp32 partial of this k split; splitk_finalize adds the splits, bias and activation
         float* w = reinterpret_cast<float*>(d.aux) + ((int64_t)d.sbase + kt0 / (int)d.kper) * M * N;
@@ -2167,6 +2263,16 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     }
         TL(64) TL(128) TL(160) TL(192)
 #undef TL
+        SERANN_CHECK(hipGetLastError());
+        return;
+    }
+    if (mode == MODE_DGRAD && variant > 17000 && variant < 19000) {
+        // GF_NBNSUM: the BN-backward-sums epilogue (17000 + BN: transposed weights, 18000 + BN: natural)
+#define TLS(BN_)                                                                                                \
+    if (variant == 17000 + BN_) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_, false, true>), grid, block, 0, s, dp, tp); \
+    else if (variant == 18000 + BN_) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_, true, true>), grid, block, 0, s, dp, tp);
+        TLS(64) TLS(128) TLS(160) TLS(192)
+#undef TLS
         SERANN_CHECK(hipGetLastError());
         return;
     }

@@ -268,12 +268,67 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
     }
 }
 
+// Phase 6: the BN backward + Dense WGRAD of a K = 1 pair whose consumer DGRAD reduced the per-column sums into
+// NbnDesc::part (gemm3.hip g3_tiled_kernel, GF_NBNSUM) -- the replacement of phases 4 and 5, which re-read the
+// stored dY twice.  With gg = gamma * invstd, ma = sum(dy) / R, mb = sum(dy xhat) / R, the BN backward is
+//   dz = a * gg * (dy - mb xhat - ma)          (a = act'(y); nbn.hip phase 5 forms the same dz per element)
+// so dW = gg (S[a x dy] - mb S[a x xhat] - ma S[a x]), db = gg (S[a dy] - mb S[a xhat] - ma S[a]),
+// dgamma = S[dy xhat], dbeta = S[dy].  A block owns NBN_FIN_CH channels of one problem; thread (channel, sum,
+// position quarter) adds its slots over m tiles and positions in a fixed order (fp64), the quarters are then
+// added in order: bitwise reproducible.
+constexpr int NBN_FIN_CH = 8, NBN_FIN_PARTS = 4;
+__global__ __launch_bounds__(256) void nbn_fin_kernel(const NbnDesc* __restrict__ descs, const int4* __restrict__ tiles) {
+    __shared__ double tot[NBN_FIN_PARTS][NBN_FIN_CH * NBN_NSUM];
+    const int4 td = tiles[blockIdx.x];                 // (problem, first channel, 0, 0)
+    const NbnDesc& d = descs[td.x];
+    const int F = (int)d.F, np = (int)d.np, mt = (int)d.mtiles;
+    const int64_t N = (int64_t)np * F;
+    const int f0 = td.y, nch = min(NBN_FIN_CH, F - f0);
+    const float* __restrict__ part = reinterpret_cast<const float*>(d.part);
+    const int t = threadIdx.x, slot = t & (NBN_FIN_CH * NBN_NSUM - 1), q = t / (NBN_FIN_CH * NBN_NSUM);
+    static_assert(NBN_FIN_CH * NBN_NSUM * NBN_FIN_PARTS == 256, "one thread per (channel, sum, position part)");
+    double v = 0.0;
+    if (slot < nch * NBN_NSUM) {
+        const int u = f0 * NBN_NSUM + slot;            // (channel f0 + slot / 8, sum slot % 8): contiguous
+        const int pa = q * np / NBN_FIN_PARTS, pb = (q + 1) * np / NBN_FIN_PARTS;
+        for (int m = 0; m < mt; ++m) {
+            const float* pm = part + (int64_t)m * N * NBN_NSUM + u;
+#pragma unroll 4
+            for (int p = pa; p < pb; ++p) v += (double)pm[(int64_t)p * F * NBN_NSUM];
+        }
+    }
+    tot[q][slot] = v;
+    __syncthreads();
+    if (t < nch) {
+        const int f = f0 + t;
+        double S[NBN_NSUM];
+#pragma unroll
+        for (int k = 0; k < NBN_NSUM; ++k) {
+            S[k] = 0.0;
+#pragma unroll
+            for (int pq = 0; pq < NBN_FIN_PARTS; ++pq) S[k] += tot[pq][t * NBN_NSUM + k];   // fixed order
+        }
+        const double Rf = (double)d.R;
+        const double is = reinterpret_cast<const float*>(d.invstd)[f];
+        const double gg = ((d.flags & 1) ? (double)reinterpret_cast<const float*>(d.gamma)[f] : 1.0) * is;
+        const double ma = S[0] / Rf, mb = S[1] / Rf;
+        if (d.flags & 1) fx_add(reinterpret_cast<long long*>(d.dgamma) + f, (float)S[1]);
+        if (d.flags & 2) fx_add(reinterpret_cast<long long*>(d.dbeta) + f, (float)S[0]);
+        fx_add(reinterpret_cast<long long*>(d.dw) + f, (float)(gg * (S[5] - mb * S[6] - ma * S[7])));
+        if (d.db) fx_add(reinterpret_cast<long long*>(d.db) + f, (float)(gg * (S[2] - mb * S[3] - ma * S[4])));
+    }
+}
+
 void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
     const dim3 grid((unsigned)ntiles), block(256);
     hipStream_t s = as_stream(stream);
     const NbnDesc* dp = as_ptr<const NbnDesc>(descs);
     const int4* tp = as_ptr<const int4>(tiles);
+    if (phase == 6) {
+        hipLaunchKernelGGL(nbn_fin_kernel, grid, block, 0, s, dp, tp);
+        return;
+    }
 #define NBN_CASE(P_, K_) \
     if (phase == P_ && k == K_) { hipLaunchKernelGGL((nbn_kernel<P_, K_>), grid, block, 0, s, dp, tp); return; }
 #define NBN_K(K_) NBN_CASE(2, K_) NBN_CASE(4, K_) NBN_CASE(5, K_)

@@ -19,6 +19,7 @@ struct GemmDesc {
     int64_t sbase;    // GF_SPLITWS: first workspace slot of this problem (K slices of one output share a workspace)
     int64_t ldo;      // WGRAD (64-row LDS kernel): output row stride (0: N) -- a column slice of a wider dW
     int64_t adam;     // GF_ADAM: device AdamCtx of the parameter arenas (WGRAD applies Adam to its tile)
+    int64_t ext;      // GF_NBNSUM: device NbnDesc of the fused raw-input Dense -> BN pair whose dY this DGRAD is
 };
 // The parameter / gradient / moment arenas of a population engine (same layout, element e of each is the
 // same parameter) and the device Adam scalars, for WGRAD epilogues that apply the optimizer step (GF_ADAM).
@@ -41,6 +42,10 @@ enum GemmFlags : int64_t {
                           // epilogue instead of storing the gradient; the arena-wide Adam pass skips it
     GF_NOSTORE = 32,      // FWD narrow kernel with GF_BNSTAT: statistics only, the output is never stored
                           // (its only consumer recomputes it: nbn.hip)
+    GF_NBNSUM = 512,      // DGRAD (LDS-tiled kernel) producing the output gradient of a fused raw-input
+                          // Dense (1 input channel) -> BN pair (ext = its NbnDesc): instead of storing dY, reduce the BN / Dense
+                          // backward sums of every column over the block's rows into NbnDesc::part; nbn
+                          // phase 6 finishes them (nbn.hip)
 };
 enum GemmMode : int { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
@@ -138,7 +143,11 @@ struct NbnDesc {
     int64_t x, w, bias, y, dy, gamma, beta, mm, mv, mean, invstd, ws, wsb, dw, db, dgamma, dbeta;
     int64_t R, F, K, ldx, act, flags;
     double eps, momentum;
+    // GF_NBNSUM / phase 6 (K = 1 pairs): fp32 partial sums [mtiles][N][NBN_NSUM] written by the consumer's
+    // DGRAD epilogue, one slot per 128-row m tile (N = np * F columns; BN row of (m, n) = m * np + n / F)
+    int64_t part, mtiles, np;
 };
+constexpr int NBN_NSUM = 8;
 // nbn tiles (int4): (problem, first super-row, end super-row, 1 for the problem's first block); the planner
 // sizes the ranges (hip_ops.nbn_tiles)
 void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float b2, uint64_t stream);

@@ -120,6 +120,8 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
 
 
 FUSE_NBN = os.environ.get("SERANN_FUSE_NBN", "1") != "0"
+# fused pairs whose BN output feeds one LDS-tiled DGRAD: BN backward sums in that DGRAD's epilogue (nbn phase 6)
+NBN_SUM = os.environ.get("SERANN_NBNSUM", "1") != "0"
 
 
 def nbn_pairs(ir: OrganismIR) -> Dict[int, int]:
@@ -862,6 +864,49 @@ class HipPopulationEngine(PopulationEngine):
         # fused raw-input Dense -> BatchNormalization (training): BN id -> Dense id, and the Dense ids
         nbn = [nbn_pairs(lay.ir) if train and (sel is None or o in sel) else {} for o, lay in enumerate(self.layouts)]
         nbn_src = [set(m.values()) for m in nbn]
+        # pairs whose BN output has ONE consumer GEMM, whose DGRAD runs on the LDS-tiled kernel: that DGRAD reduces
+        # the BN / Dense backward sums in its epilogue (GF_NBNSUM) instead of storing dY, and nbn phase 6 replaces
+        # phases 4 and 5 (which read the stored dY twice)
+        nbnsum = [set() for _ in range(P)]
+        if train and NBN_SUM and "tiled" not in H._OFF:
+            for o, lay in org_iter():
+                ir = lay.ir
+                owner = mem["orgs"][o]["owner"]
+                for bid, did in nbn[o].items():
+                    if ir.node(did).attrs["cin"] != 1:
+                        continue                        # the DGRAD epilogue form covers 1-channel raw inputs
+                    uses = [n for n in ir.nodes if n.op != "reshape" and any(owner.get(i, i) == bid for i in n.inputs)]
+                    if len(uses) != 1:
+                        continue
+                    u = uses[0]
+                    if u.op == "concat" and u.id in fcat[o]:
+                        cons = [g for g, c in fcons[o].items() if c == u.id]
+                        if len(cons) != 1 or sum(owner.get(pid, pid) == bid for pid, _, _ in fcat[o][u.id]) != 1:
+                            continue
+                        cn = ir.node(cons[0])
+                        kdg = ir.num_classes + ir.genotype_size if cn.attrs["kind"] == "head_cls" else cn.attrs["f"]
+                        ok = kdg > H.BK
+                    elif (u.op == "gemm" and u.attrs["kind"] == "dense" and owner.get(u.inputs[0], u.inputs[0]) == bid):
+                        a_ = u.attrs
+                        ok = a_["kh"] * a_["kw"] == 1 and a_["sh"] * a_["sw"] == 1 and a_["f"] > H.BK
+                    else:
+                        ok = False
+                    if ok:
+                        nbnsum[o].add(bid)
+        nbnsum_rows = [dict() for _ in range(P)]
+
+        def nbnsum_ext(o, bid, M_, N_):
+            """Device NbnDesc (with its partial-sum workspace) for the GF_NBNSUM DGRAD of pair ``bid``."""
+            row = nbn_row(o, bid)
+            Fb = int(row["F"])
+            if N_ % Fb:
+                raise RuntimeError(f"organism {o}: BN {bid} gradient columns {N_} not a multiple of its {Fb} channels")
+            mt = -(-M_ // 128)                          # the LDS-tiled kernel's m tile
+            part = torch.empty(mt * N_ * H.NBN_NSUM, dtype=torch.float32, device=self.device)
+            plan.keep.append(part)
+            row.update(part=part.data_ptr(), mtiles=mt, np=N_ // Fb)
+            nbnsum_rows[o][bid] = row
+            return desc_tensor([row], H.NBN_DTYPE).data_ptr()
 
         def nbn_row(o, bid):
             lay_ = self.layouts[o]
@@ -893,7 +938,8 @@ class HipPopulationEngine(PopulationEngine):
                 by_k.setdefault(int(r["K"]), []).append(r)
             for k_ in sorted(by_k):
                 rws = by_k[k_]
-                tiles = H.nbn_tiles([(r["R"], r["F"]) for r in rws], phase)
+                tiles = H.nbn_fin_tiles([r["F"] for r in rws]) if phase == 6 else \
+                    H.nbn_tiles([(r["R"], r["F"]) for r in rws], phase)
                 if len(tiles):
                     plan.launches.append(Launch("nbn", (phase, k_), desc_tensor(rws, H.NBN_DTYPE), T(tiles),
                                                 len(tiles)))
@@ -1201,7 +1247,7 @@ class HipPopulationEngine(PopulationEngine):
             bn_red, bn_red_cnt = [], []
             cpw_rows = []
             gcb_rows = []
-            nbnb_rows = []
+            nbnb_rows, nbnf_rows = [], []
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             ew_bpre = []                        # non-last-axis BN: dy -> channels-last dyt
             for o, lay in org_iter():
@@ -1220,7 +1266,10 @@ class HipPopulationEngine(PopulationEngine):
                     if not rec["req"].get(n.id, False) or n.id in rec["fused_convs"] or n.id in nbn_src[o]:
                         continue
                     if n.op == "bn" and n.id in nbn[o]:
-                        nbnb_rows.append(nbn_row(o, n.id))     # BN backward + the Dense's WGRAD (nbn.hip)
+                        if n.id in nbnsum_rows[o]:
+                            nbnf_rows.append(nbnsum_rows[o][n.id])   # sums reduced by the consumer's DGRAD
+                        else:
+                            nbnb_rows.append(nbn_row(o, n.id))     # BN backward + the Dense's WGRAD (nbn.hip)
                         continue
                     if n.op == "pool" and n.id in cpool[o]:
                         # fused pool backward + conv WGRAD + bias gradient (no DGRAD: raw image input)
@@ -1266,7 +1315,11 @@ class HipPopulationEngine(PopulationEngine):
                                                 _bnat=wptr_bf(lay.w[n.id]) + 2 * col, _bnat_ld=D,
                                                 aux=yv, act=act, out=mem["grad"].ptr(rec["grad"][own_p]), H=Hh, W=1,
                                                 C=width, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=width, K=F)
-                                    tasks["dgrad"].append((o, own_p, lambda acc, r=base: dict(r, flags=H.GF_ACCUM if acc else 0),
+                                    sf = 0
+                                    if own_p in nbnsum[o]:
+                                        base["ext"] = nbnsum_ext(o, own_p, M, width)
+                                        sf = H.GF_NBNSUM
+                                    tasks["dgrad"].append((o, own_p, lambda acc, r=base, sf=sf: dict(r, flags=(H.GF_ACCUM if acc else 0) | sf),
                                                            (M, width, F)))
                             continue
                         if ic is not None:
@@ -1288,7 +1341,11 @@ class HipPopulationEngine(PopulationEngine):
                                         out=mem["grad"].ptr(rec["grad"][own]), H=Hh,
                                         W=Ww, C=C, OH=OH, OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=Mi, N=C,
                                         K=KH * KW * F)
-                            tasks["dgrad"].append((o, own, lambda acc, r=base, v=vec: dict(r, flags=v | (H.GF_ACCUM if acc else 0)),
+                            sf = 0
+                            if own in nbnsum[o]:
+                                base["ext"] = nbnsum_ext(o, own, Mi, C)
+                                sf = H.GF_NBNSUM
+                            tasks["dgrad"].append((o, own, lambda acc, r=base, v=vec, sf=sf: dict(r, flags=v | sf | (H.GF_ACCUM if acc else 0)),
                                                    (Mi, C, KH * KW * F)))
                     elif n.op == "pool":
                         own = target(o, n.inputs[0])
@@ -1398,6 +1455,7 @@ class HipPopulationEngine(PopulationEngine):
                 add_chunked("bn", 4, bn_red, H.BN_DTYPE, bn_red_cnt, 1)
             add_nbn(nbnb_rows, 4)
             add_nbn(nbnb_rows, 5)
+            add_nbn(nbnf_rows, 6)
             for stage in STAGES:
                 batches = [[]]
                 used = [set()]
@@ -1701,6 +1759,7 @@ class HipPopulationEngine(PopulationEngine):
                           self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), c.lr, c.beta1, c.beta2, c.eps, s)
         torch.cuda.synchronize(dev)
         self._debug_mem = mem
+        self._debug_plan = plan                          # (tests inspect its launches)
         return grads, H.from_q32(metrics)
 
     def debug_logits(self, mem=None) -> List[np.ndarray]:
@@ -1842,7 +1901,7 @@ class HipPopulationEngine(PopulationEngine):
             torch.cuda.synchronize(self.device)
         self.graph = None
         self.plans.clear()
-        for name in ("_fit_bufs", "_train_mem", "_train_mem_rem", "_debug_mem", "_adam_skip", "_adam_ctx", "_streams"):
+        for name in ("_fit_bufs", "_train_mem", "_train_mem_rem", "_debug_mem", "_debug_plan", "_adam_skip", "_adam_ctx", "_streams"):
             if hasattr(self, name):
                 delattr(self, name)
 

@@ -21,7 +21,8 @@ GEMM_FIELDS = ["a", "b", "out", "bias", "aux", "H", "W", "C", "OH", "OW", "F", "
                "ldb",       # LDS-tiled kernel: B row stride (0: K)
                "sbase",     # GF_SPLITWS: first workspace slot
                "ldo",       # 64-row WGRAD: output row stride (0: N)
-               "adam"]      # GF_ADAM: device AdamCtx
+               "adam",      # GF_ADAM: device AdamCtx
+               "ext"]       # GF_NBNSUM: device NbnDesc of the fused Dense -> BN pair
 GEMM_DTYPE = np.dtype([(f, _I) for f in GEMM_FIELDS])
 BN_DTYPE = np.dtype([(f, _I) for f in ["x", "y", "dy", "dx", "gamma", "beta", "mm", "mv", "mean", "invstd", "ws",
                                        "dgamma", "dbeta", "pdb", "R", "C", "flags"]] + [("eps", np.float64),
@@ -50,6 +51,7 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
                       + [("lb", np.float64)])
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 64, 128
+GF_NBNSUM = 512
 GF_NOSTORE = 32
 GF_ADAM = 256
 ADAM_CTX_DTYPE = np.dtype([(f, _I) for f in ['p', 'm', 'v', 'pbf', 'g', 'lr_t']] + [(f, np.float32) for f in ['b1', 'b2', 'eps', 'pad']])
@@ -111,7 +113,8 @@ BN_VEC_ELEMS = 16384   # aux.hip: elements per block of the vectorised (C <= 256
 
 NBN_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "dy", "gamma", "beta", "mm", "mv", "mean", "invstd",
                                         "ws", "wsb", "dw", "db", "dgamma", "dbeta", "R", "F", "K", "ldx", "act",
-                                        "flags"]] + [("eps", np.float64), ("momentum", np.float64)])
+                                        "flags"]] + [("eps", np.float64), ("momentum", np.float64)]
+                     + [(f, _I) for f in ["part", "mtiles", "np"]])
 # nbn.hip block sizes: elements per block of phase 2 (a streaming write; each block first rebuilds the
 # per-channel scale / shift from the statistics workspace, so short blocks pay that prologue often), and
 # the multiple of it taken by the reduction phases 4 / 5
@@ -129,6 +132,16 @@ def nbn_super_rows(units: int, phase: int) -> int:
 def nbn_chunks(rows: int, units: int, phase: int) -> int:
     """Blocks of a fused raw-input Dense -> BatchNormalization problem [rows][units] (nbn.hip)."""
     return -(-(-(-int(rows) // 8)) // nbn_super_rows(units, phase))
+
+
+NBN_FIN_CH = 8      # nbn.hip nbn_fin_kernel: channels per block
+NBN_NSUM = 8        # serann_hip.h: GF_NBNSUM sums per column
+
+
+def nbn_fin_tiles(channels) -> np.ndarray:
+    """int32 (ntiles, 4) tile table of an nbn phase-6 launch: (problem, first channel, 0, 0)."""
+    out = [(p, f0, 0, 0) for p, F in enumerate(channels) for f0 in range(0, int(F), NBN_FIN_CH)]
+    return np.asarray(out, dtype=np.int32).reshape(-1, 4)
 
 
 def nbn_tiles(rows_units, phase: int) -> np.ndarray:
@@ -478,10 +491,10 @@ def gemm3_block(mode: int, variant: int):
     if mode == MODE_WGRAD:
         v = variant % 1000000
         return (v // 1000, (v % 1000) % 500)
-    if 7000 < variant < 7300:
-        return (128, variant - 7000)
-    if 8000 < variant < 8300:
-        return (128, variant - 8000)
+    if 7000 < variant % 10000 < 7300 and variant < 20000:
+        return (128, variant % 10000 - 7000)
+    if 8000 < variant % 10000 < 8300 and variant < 20000:
+        return (128, variant % 10000 - 8000)
     if variant >= 5000:
         return (64 * ((variant // 10) % 10), 16 * (variant % 10))
     nt, rt, kw = variant % 10, (variant // 10) % 10, (variant % 1000) >= 100
@@ -640,6 +653,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 v += 1000
                 r["b"] = r["_bnat"]
                 r["ldb"] = int(r.get("_bnat_ld", 0))
+            if mode == MODE_DGRAD and int(r.get("flags", 0)) & GF_NBNSUM:
+                v += 10000                        # the instantiation with the BN-backward-sums epilogue
             if mode == MODE_FWD and splitk:
                 # (split count from the problem's own column tile, not the launch's shared width below:
                 # the split boundaries decide the fp32 partial sums, so they must not depend on the

@@ -106,6 +106,15 @@ ARCHS = {
         "con = Dense(units=24, activation='relu')(con)\n\nloss_balance = 0.7"),
     # fused raw-input Dense -> BatchNormalization (csrc/hip/nbn.hip): a linear 8-unit image Dense, a
     # 200-unit sigmoid genotype Dense (one super-row group per block), a Dense after the BN
+    # fused Dense -> BN whose BN output feeds one Dense directly (not through a concat) on the LDS-tiled DGRAD:
+    # the BN backward sums are reduced in that DGRAD's epilogue (GF_NBNSUM, nbn phase 6).  (relu: a sigmoid of
+    # the 0/1 genotype has a ~0.07 spread per channel, which the BN turns into an ill-conditioned parity case)
+    "nbn_sum_direct": (
+        "g_layer = Dense(units=64, activation='relu')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n"
+        "g_layer = Dense(units=48, activation='relu')(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=40, activation='relu')(con)\n\nloss_balance = 0.5"),
     "nbn_wide_linear": (
         "X_layer = Dense(units=8)(X_layer)\n"
         "X_layer = BatchNormalization()(X_layer)\n\n"

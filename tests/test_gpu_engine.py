@@ -424,7 +424,7 @@ def test_gchain_fusion_matches_unfused(name, monkeypatch):
     assert np.allclose(acc_f, acc_p, atol=0.05), (acc_f, acc_p)
 
 
-@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_wide_linear"])
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_wide_linear", "nbn_sum_direct"])
 def test_nbn_fusion_matches_unfused(name, monkeypatch):
     """Fused raw-input Dense -> BatchNormalization (nbn.hip: the Dense output is recomputed from the raw
     input in every pass, dz stays fp32) against the unfused narrow GEMM + BN kernels: logits, every
@@ -465,6 +465,40 @@ def test_nbn_fusion_matches_unfused(name, monkeypatch):
     acc_f = fused.evaluate(x, labels, g, cfg)
     acc_p = plain.evaluate(x, labels, g, cfg)
     assert np.allclose(acc_f, acc_p, atol=0.03), (acc_f, acc_p)
+
+
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_sum_direct"])
+def test_nbn_sums_in_dgrad_match_phases_4_5(name, monkeypatch):
+    """The BN backward of a fused raw-input Dense -> BN pair reduced in its consumer's DGRAD epilogue
+    (GF_NBNSUM + nbn phase 6, dY never stored) against nbn phases 4 / 5 over the stored bf16 dY: the plan uses
+    the fused form, and every gradient is at least as close to the fp32 oracle (1.25x + 1 % slack), at the
+    production batch."""
+    from serann.engine import hip_engine as he
+    from serann.ops import hip_ops as H
+    ir = interpret(ARCHS[name])
+    params = init_params(ir, 3)
+    x, g, y = _batch(750, seed=2)
+    fused = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, _ = fused.debug_train_step(x, g, y)
+    kinds = [(la.kind, la.arg) for la in fused._debug_plan.launches]
+    assert any(k == "nbn" and a[0] == 6 for k, a in kinds), kinds
+    assert not any(k == "nbn" and a[0] in (4, 5) for k, a in kinds), kinds
+    assert any(k == "gemm3" and a[0] == H.MODE_DGRAD and 17000 < a[1] < 19000 for k, a in kinds), kinds
+    monkeypatch.setattr(he, "NBN_SUM", False)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, _ = plain.debug_train_step(x, g, y)
+    assert any(k == "nbn" and a[0] == 5 for k, a in [(la.kind, la.arg) for la in plain._debug_plan.launches])
+    _, ref = _oracle(ir, params, x, g, y)
+    a, b = fused.export_arena(0, gf), plain.export_arena(0, gp)
+    gmax = max(float(np.abs(v).max()) for d in ref.values() for v in d.values())
+    for nid in ref:
+        for k in ref[nid]:
+            r = np.asarray(ref[nid][k], np.float64)
+            ef, eu = np.linalg.norm(a[nid][k] - r), np.linalg.norm(b[nid][k] - r)
+            floor = 1e-3 * gmax * np.sqrt(r.size)
+            assert ef < 1.25 * eu + 0.01 * np.linalg.norm(r) + floor, (name, nid, k, ef, eu, np.linalg.norm(r))
+    fused.close()
+    plain.close()
 
 
 def test_adam_kernel_matches_keras_formula():
