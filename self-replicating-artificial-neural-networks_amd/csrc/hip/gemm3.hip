@@ -27,7 +27,10 @@
 #include "serann_hip.h"
 
 #ifndef WG_NSETS
-#define WG_NSETS 2          // WGRAD register sets in flight (build-time A/B knob)
+// WGRAD register sets in flight (build-time A/B knob).  One set: 127 VGPRs, 3 waves per SIMD; two sets (the
+// round-2 choice): 183 + 36 AGPRs, 2 waves -- one set measured 5.6 vs 5.9 ms (ancestor) and 13.7 vs 13.9 ms
+// (generation-3 mix, 4 stream groups) per step (profiles/r4/ab_wgrad_nsets1.txt)
+#define WG_NSETS 1
 #endif
 #ifndef WG_WAVES_PER_EU
 #define WG_WAVES_PER_EU 0   // WGRAD occupancy target (build-time A/B knob; 0: the compiler's choice)
@@ -1815,6 +1818,8 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
 // columns (16-B chunks along n), staged k-major in LDS ([32][BN + 8]) and its MFMA fragments are read
 // with ds_read_b64_tr_b16 (lane i of a 16-lane group receives column i of 4 consecutive k rows, k row q
 // in element q -- the k order of the ds_read_b128 A fragments).  No per-step weight transpose launch.
+// (Occupancy: requesting 3 waves per SIMD for BN <= 160 -- accumulators in VGPRs, no spills -- measured 2-3 %
+// slower on the ancestor population and neutral on the generation-3 mix: profiles/r4/ab_tiled_occupancy.txt)
 template <int MODE, int BN, bool BT = false, bool NS = false>
 __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restrict__ descs,
                                                        const int4* __restrict__ tiles) {
