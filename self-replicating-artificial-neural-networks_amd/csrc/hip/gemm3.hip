@@ -293,7 +293,11 @@ __device__ __forceinline__ void wave_store_rows(bf16_t* __restrict__ st, bf16_t*
 //   KW = true : block = RT*16 rows; the 4 waves split the k range (k-steps w, w+4, ...) and reduce
 //               their accumulators through LDS -- for few-row / long-K problems (merged Dense, heads).
 template <int MODE, int NT, int RT, bool KW, bool GEN, bool SK = false>
-__global__ __launch_bounds__(256) void g3_direct_kernel(const GemmDesc* __restrict__ descs,
+// Occupancy request by tile size (NT x RT 16-column x 64-row fragments per wave): without it the compiler parks
+// accumulators in AGPRs and settles one wave per SIMD lower (e.g. <1, 8, 2>: 138 + 128 registers, 1 wave; with
+// it 202, 2 waves; no spills).  Generation-3 mix: 13.73 -> 13.65 ms per step (profiles/r4/ab_direct_occupancy.txt)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT * RT >= 16 ? 2 : (NT * RT >= 8 ? 3 : 4))))
+void g3_direct_kernel(const GemmDesc* __restrict__ descs,
                                                         const int4* __restrict__ tiles) {
     constexpr int WROWS = RT * 16;
     constexpr int BMB = KW ? WROWS : 4 * WROWS, BNB = NT * 16;
