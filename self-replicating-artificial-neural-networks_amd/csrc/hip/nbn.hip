@@ -274,10 +274,10 @@ __global__ __launch_bounds__(256) void nbn_kernel(const NbnDesc* __restrict__ de
 //   dz = a * gg * (dy - mb xhat - ma)          (a = act'(y); nbn.hip phase 5 forms the same dz per element)
 // so dW = gg (S[a x dy] - mb S[a x xhat] - ma S[a x]), db = gg (S[a dy] - mb S[a xhat] - ma S[a]),
 // dgamma = S[dy xhat], dbeta = S[dy].  A block owns NBN_FIN_CH channels of one problem; thread (channel, sum,
-// position quarter) adds its slots over m tiles and positions in a fixed order (fp64), the quarters are then
-// added in order: bitwise reproducible.
-constexpr int NBN_FIN_CH = 8, NBN_FIN_PARTS = 4;
-__global__ __launch_bounds__(256) void nbn_fin_kernel(const NbnDesc* __restrict__ descs, const int4* __restrict__ tiles) {
+// part) adds a fixed share of the (m tile, position) slots in a fixed order (fp64), the parts are then added in
+// order: bitwise reproducible.
+constexpr int NBN_FIN_CH = 8, NBN_FIN_PARTS = 16;
+__global__ __launch_bounds__(1024) void nbn_fin_kernel(const NbnDesc* __restrict__ descs, const int4* __restrict__ tiles) {
     __shared__ double tot[NBN_FIN_PARTS][NBN_FIN_CH * NBN_NSUM];
     const int4 td = tiles[blockIdx.x];                 // (problem, first channel, 0, 0)
     const NbnDesc& d = descs[td.x];
@@ -286,15 +286,18 @@ __global__ __launch_bounds__(256) void nbn_fin_kernel(const NbnDesc* __restrict_
     const int f0 = td.y, nch = min(NBN_FIN_CH, F - f0);
     const float* __restrict__ part = reinterpret_cast<const float*>(d.part);
     const int t = threadIdx.x, slot = t & (NBN_FIN_CH * NBN_NSUM - 1), q = t / (NBN_FIN_CH * NBN_NSUM);
-    static_assert(NBN_FIN_CH * NBN_NSUM * NBN_FIN_PARTS == 256, "one thread per (channel, sum, position part)");
+    static_assert(NBN_FIN_CH * NBN_NSUM * NBN_FIN_PARTS == 1024, "one thread per (channel, sum, part)");
     double v = 0.0;
     if (slot < nch * NBN_NSUM) {
+        // the (m tile, position) slots of this (channel, sum), flattened and dealt round-robin to the parts:
+        // each thread adds its share in a fixed order (a direct consumer has np = 1 and hundreds of m tiles,
+        // the fused-concat one np = 100 and a few)
         const int u = f0 * NBN_NSUM + slot;            // (channel f0 + slot / 8, sum slot % 8): contiguous
-        const int pa = q * np / NBN_FIN_PARTS, pb = (q + 1) * np / NBN_FIN_PARTS;
-        for (int m = 0; m < mt; ++m) {
-            const float* pm = part + (int64_t)m * N * NBN_NSUM + u;
+        const int total = mt * np;
 #pragma unroll 4
-            for (int p = pa; p < pb; ++p) v += (double)pm[(int64_t)p * F * NBN_NSUM];
+        for (int i = q; i < total; i += NBN_FIN_PARTS) {
+            const int m = i / np, p = i - m * np;
+            v += (double)part[((int64_t)m * N + (int64_t)p * F) * NBN_NSUM + u];
         }
     }
     tot[q][slot] = v;
@@ -326,7 +329,7 @@ void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles
     const NbnDesc* dp = as_ptr<const NbnDesc>(descs);
     const int4* tp = as_ptr<const int4>(tiles);
     if (phase == 6) {
-        hipLaunchKernelGGL(nbn_fin_kernel, grid, block, 0, s, dp, tp);
+        hipLaunchKernelGGL(nbn_fin_kernel, grid, dim3(1024), 0, s, dp, tp);
         return;
     }
 #define NBN_CASE(P_, K_) \
