@@ -833,6 +833,34 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const SplitFinDesc
     const bool f32 = d.flags & 1;
     const int64_t e0 = (int64_t)td.y * SPLITFIN_ELEMS;
     const int64_t e1 = min(MN, e0 + SPLITFIN_ELEMS);
+    // 4 consecutive elements per thread (16-B partial loads, 8- / 16-B stores) when the slabs allow it; the
+    // column index advances incrementally (no 64-bit modulo per element).  Splits are added in order.
+    if ((MN & 3) == 0 && ((d.ws | d.out) & 15) == 0) {
+        int64_t e = e0 + 4 * threadIdx.x;
+        int col = (int)(e % N);
+        const int step = (int)(1024 % N);
+        for (; e < e1; e += 1024) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int s_ = 0; s_ < S; ++s_) {
+                const float4 w = *reinterpret_cast<const float4*>(ws + s_ * MN + e);
+                v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+            }
+            float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                int c = col + j;
+                if (c >= N) c -= N;
+                if (c >= N) c %= N;                   // N < 4
+                if (bias) r[j] += bias[c];
+                r[j] = apply_act(r[j], act);
+            }
+            if (f32) *reinterpret_cast<float4*>(out32 + e) = make_float4(r[0], r[1], r[2], r[3]);
+            else *reinterpret_cast<uint2*>(out + e) = make_uint2(f2bf2(r[0], r[1]), f2bf2(r[2], r[3]));
+            col += step;
+            if (col >= N) col -= N;
+        }
+        return;
+    }
     for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
         float v = 0.f;
         for (int s_ = 0; s_ < S; ++s_) v += ws[s_ * MN + e];
