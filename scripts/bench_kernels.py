@@ -107,7 +107,6 @@ def main():
     xb = torch.rand(B, 784, device=dev).bfloat16()
     gb = torch.randint(0, 2, (B, 100), device=dev).bfloat16()
     yb = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
-    eng._input_tensors = {xb.data_ptr(): xb, gb.data_ptr(): gb}
     metrics = torch.zeros(len(irs), 4, dtype=torch.int64, device=dev)
     inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in irs]
     plan = eng._build_plan("train", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * len(irs), metrics)
