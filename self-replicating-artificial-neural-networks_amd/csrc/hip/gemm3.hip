@@ -23,6 +23,8 @@
 //   WGRAD : dWm[f][k] += sum_m dZ[m][f] . im2col(X)[m][k]      (LDS tiles, transposing LDS reads,
 //           64 rows of m per barrier pair, Q32 fixed-point atomics into the gradient arena for split-m)
 // dZ = dY * act'(Y) is formed on the fly from the layer output Y (GemmDesc::aux) in DGRAD / WGRAD.
+#include <type_traits>
+
 #include "common.h"
 #include "serann_hip.h"
 
@@ -1833,8 +1835,8 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     constexpr int ABYTES = 2 * BM * LDS_ROW, BBYTES = BT ? 2 * BK * LDBT : 2 * BN * LDS_ROW;
     constexpr int STAGE = BM * (BN + 8);             // epilogue staging (bf16 elements, padded rows)
     constexpr int LDSN0 = (ABYTES + BBYTES) > STAGE ? (ABYTES + BBYTES) : STAGE;
-    // NS epilogue staging (floats): x tile [BM][BN / 8 + 2], dY slice [BM][33], wave sums [4][32][8]
-    constexpr int NSLDS = NS ? 2 * (BM * (BN / 8 + 2) + BM * 33 + 4 * 32 * 8) : 0;
+    // NS epilogue staging (floats): x tile [BN / 8 + 2][BM + 4], dY slice [32][BM + 4], sums [2][8][32][8]
+    constexpr int NSLDS = NS ? 2 * ((BN / 8 + 2) * (BM + 4) + 32 * (BM + 4) + 2 * 8 * 32 * 8) : 0;
     constexpr int LDSN = LDSN0 > NSLDS ? LDSN0 : NSLDS;
     __shared__ __attribute__((aligned(16))) bf16_t lds[LDSN];
     bf16_t* As = lds;                                // [2][BM][LDS_ROW]
@@ -1993,26 +1995,82 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         // per column tile j the fp32 dY slice [BM][32] (both waves along n): the sums are then formed from LDS
         // by (column, 16-row group) threads -- reading the accumulators in place would keep the whole tile
         // in VGPRs through the epilogue, and that peak (not the k loop) would set the occupancy
-        constexpr int SLD = 33;                          // slice row stride (floats): conflict-free column reads
+        // Layouts are column-major so that every LDS access is a 16-B vector: the accumulators' 4 consecutive
+        // rows go out as one ds_write_b128 and a (column, 16-row group) thread reads its rows as 4 of them;
+        // strides of BM + 4 floats put the 16 lanes of a b128 group on distinct banks
+        constexpr int SLT = BM + 4;
         const int p0 = n0 / Fb, npos = min(N - 1, n0 + BN - 1) / Fb - p0 + 1;
-        float* xs = reinterpret_cast<float*>(lds);       // [BM][npos]; the k loop ended on a barrier
-        float* sl = xs + BM * (BN / 8 + 2);              // [BM][SLD]
-        float* red = sl + BM * SLD;                      // [4 waves][32 columns][NSUM]
-        static_assert((BM * (BN / 8 + 2) + BM * SLD + 4 * 32 * NSUM) * 4 <= LDSN * 2,
+        float* xs = reinterpret_cast<float*>(lds);       // [npos][SLT]; the k loop ended on a barrier
+        float* sl = xs + (BN / 8 + 2) * SLT;             // [32 columns][SLT]
+        float* red = sl + 32 * SLT;                      // [2 buffers][8 row groups][32 columns][NSUM]
+        static_assert(((BN / 8 + 2) * SLT + 32 * SLT + 2 * 8 * 32 * NSUM) * 4 <= LDSN * 2,
                       "NBNSUM staging must fit in the LDS tiles");
         for (int u = t; u < BM * npos; u += 256) {
-            const int rl = u / npos, pp = u - rl * npos;
+            const int pp = u / BM, rl = u - pp * BM;
             const int row = min(m0 + rl, M - 1);
-            xs[u] = bf2f(Xr[((int64_t)row * NPc + p0 + pp) * ldxr]);
+            xs[pp * SLT + rl] = bf2f(Xr[((int64_t)row * NPc + p0 + pp) * ldxr]);
         }
         float* __restrict__ part = reinterpret_cast<float*>(nd.part) + (int64_t)td.y * N * NSUM;
         const int sc = t & 31, sg = t >> 5;              // column of the slice, 16-row group
+        // rows past M: their dY is 0 (the A loads returned zeros) and their act' is masked below, so every
+        // sum gets exact zeros from them.  Activation and the full-rows case are compile-time in the row
+        // loop; the rows are taken in pairs so the sums issue as packed fp32 (v_pk_fma_f32)
+        const int nrow = M - m0 - sg * 16;
+        auto col_sums = [&](auto act_tag, auto full_tag, const float* xc, const float* gc, float w, float bv,
+                            float mu, float is, float* sm) {
+            constexpr int A = decltype(act_tag)::value;
+            constexpr bool FULL = decltype(full_tag)::value;
+            f32x2_t s[NSUM];
+#pragma unroll
+            for (int q = 0; q < NSUM; ++q) s[q] = f32x2_t{0.f, 0.f};
+            const float nmis = -mu * is;
+            // the 4 row quads stay a loop: unrolled, the hoisted LDS reads cost a wave per SIMD (112 VGPRs)
+#pragma unroll 1
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const float4 x4 = *reinterpret_cast<const float4*>(xc + 4 * r4);
+                const float4 g4 = *reinterpret_cast<const float4*>(gc + 4 * r4);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x2_t xv = h ? f32x2_t{x4.z, x4.w} : f32x2_t{x4.x, x4.y};
+                    const f32x2_t gy = h ? f32x2_t{g4.z, g4.w} : f32x2_t{g4.x, g4.y};
+                    const f32x2_t v = xv * w + bv;       // nbn.hip nbn_y: bias, then the product (one fma)
+                    f32x2_t y, a;
+                    if constexpr (A == ACT_RELU) {
+                        y = f32x2_t{v.x > 0.f ? v.x : 0.f, v.y > 0.f ? v.y : 0.f};
+                        a = f32x2_t{y.x > 0.f ? 1.f : 0.f, y.y > 0.f ? 1.f : 0.f};
+                    } else if constexpr (A == ACT_SIGMOID) {
+                        y = f32x2_t{apply_act(v.x, ACT_SIGMOID), apply_act(v.y, ACT_SIGMOID)};
+                        a = y * (1.f - y);
+                    } else {
+                        y = v;
+                        a = f32x2_t{1.f, 1.f};
+                    }
+                    if constexpr (!FULL) {
+                        const int r = 4 * r4 + 2 * h;
+                        a = f32x2_t{r < nrow ? a.x : 0.f, r + 1 < nrow ? a.y : 0.f};
+                    }
+                    const f32x2_t xh = y * is + nmis;
+                    const f32x2_t ax = a * xv;
+                    s[0] += gy;
+                    s[1] += gy * xh;
+                    s[2] += a * gy;
+                    s[3] += a * xh;
+                    s[4] += a;
+                    s[5] += ax * gy;
+                    s[6] += ax * xh;
+                    s[7] += ax;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NSUM; ++q) sm[q] = s[q].x + s[q].y;
+        };
+        const bool fullrows = m0 + BM <= M;
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) sl[(wr * 64 + i * 16 + rq + r) * SLD + wc * 16 + r16] = acc[i][j][r];
+                *reinterpret_cast<float4*>(&sl[(wc * 16 + r16) * SLT + wr * 64 + i * 16 + rq]) =
+                    make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
             __syncthreads();
             const int cl = (sc >> 4) * (BN / 2) + j * 16 + (sc & 15);   // block column of slice column sc
             const int n = n0 + cl;
@@ -2022,45 +2080,37 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             if (n < N) {
                 const int p = n / Fb, f = n - p * Fb;
                 const float w = bf2f(Wn[f]), bv = nb ? nb[f] : 0.f, mu = nmean[f], is = nis[f];
-                const float* xp = xs + (p - p0);
-#pragma unroll 4
-                for (int rr = 0; rr < 16; ++rr) {
-                    const int rl = sg * 16 + rr;
-                    if (m0 + rl >= M) break;
-                    const float xv = xp[rl * npos];
-                    float v = bv;                        // nbn.hip nbn_y: bias first, then the product
-                    v += xv * w;
-                    const float y = apply_act(v, nact);
-                    const float xh = (y - mu) * is;
-                    const float a = nact == ACT_RELU ? (y > 0.f ? 1.f : 0.f)
-                                                     : (nact == ACT_SIGMOID ? y * (1.f - y) : 1.f);
-                    const float gy = sl[rl * SLD + sc];
-                    const float ax = a * xv;
-                    sm[0] += gy;
-                    sm[1] += gy * xh;
-                    sm[2] += a * gy;
-                    sm[3] += a * xh;
-                    sm[4] += a;
-                    sm[5] += ax * gy;
-                    sm[6] += ax * xh;
-                    sm[7] += ax;
+                const float* xc = xs + (p - p0) * SLT + sg * 16;
+                const float* gc = sl + sc * SLT + sg * 16;
+                using TT = std::true_type;
+                using FT = std::false_type;
+                using RL = std::integral_constant<int, ACT_RELU>;
+                using SG = std::integral_constant<int, ACT_SIGMOID>;
+                using LN = std::integral_constant<int, ACT_LINEAR>;
+                if (fullrows) {
+                    if (nact == ACT_RELU) col_sums(RL{}, TT{}, xc, gc, w, bv, mu, is, sm);
+                    else if (nact == ACT_SIGMOID) col_sums(SG{}, TT{}, xc, gc, w, bv, mu, is, sm);
+                    else col_sums(LN{}, TT{}, xc, gc, w, bv, mu, is, sm);
+                } else {
+                    if (nact == ACT_RELU) col_sums(RL{}, FT{}, xc, gc, w, bv, mu, is, sm);
+                    else if (nact == ACT_SIGMOID) col_sums(SG{}, FT{}, xc, gc, w, bv, mu, is, sm);
+                    else col_sums(LN{}, FT{}, xc, gc, w, bv, mu, is, sm);
                 }
             }
-#pragma unroll
-            for (int q = 0; q < NSUM; ++q) sm[q] += __shfl_xor(sm[q], 32, 64);   // the wave's two row groups
-            if (lane < 32) {
-#pragma unroll
-                for (int q = 0; q < NSUM; ++q) red[(wave * 32 + sc) * NSUM + q] = sm[q];
-            }
+            // red is double-buffered: the next tile's writes cannot race this tile's reads (a barrier
+            // lies between), so one barrier per tile is saved
+            float* rb = red + (j & 1) * (8 * 32 * NSUM);
+            *reinterpret_cast<float4*>(&rb[(sg * 32 + sc) * NSUM]) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+            *reinterpret_cast<float4*>(&rb[(sg * 32 + sc) * NSUM + 4]) = make_float4(sm[4], sm[5], sm[6], sm[7]);
             __syncthreads();
             {
                 const int c2 = t / NSUM, q = t - c2 * NSUM;          // 32 columns x 8 sums = 256 threads
                 const int n2 = n0 + (c2 >> 4) * (BN / 2) + j * 16 + (c2 & 15);
-                if (n2 < N)
-                    part[(int64_t)n2 * NSUM + q] = red[c2 * NSUM + q] + red[(32 + c2) * NSUM + q] +
-                                                   red[(64 + c2) * NSUM + q] + red[(96 + c2) * NSUM + q];
+                float v = 0.f;
+#pragma unroll
+                for (int g = 0; g < 8; ++g) v += rb[(g * 32 + c2) * NSUM + q];
+                if (n2 < N) part[(int64_t)n2 * NSUM + q] = v;
             }
-            __syncthreads();                             // the slice and red are rewritten by the next tile
         }
         return;
     }

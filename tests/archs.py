@@ -115,6 +115,14 @@ ARCHS = {
         "g_layer = Dense(units=48, activation='relu')(g_layer)\n\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
         "con = Dense(units=40, activation='relu')(con)\n\nloss_balance = 0.5"),
+    # the DGRAD-epilogue BN sums (GF_NBNSUM) under the sigmoid and linear activations of the raw-input Dense
+    "nbn_sum_acts": (
+        "X_layer = Dense(units=16)(X_layer)\n"
+        "X_layer = BatchNormalization()(X_layer)\n\n"
+        "g_layer = Dense(units=64, activation='sigmoid')(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+        "con = Dense(units=48, activation='relu')(con)\n\nloss_balance = 0.5"),
     "nbn_wide_linear": (
         "X_layer = Dense(units=8)(X_layer)\n"
         "X_layer = BatchNormalization()(X_layer)\n\n"

@@ -467,7 +467,7 @@ def test_nbn_fusion_matches_unfused(name, monkeypatch):
     assert np.allclose(acc_f, acc_p, atol=0.03), (acc_f, acc_p)
 
 
-@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_sum_direct"])
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "narrow_bn_x", "nbn_sum_direct", "nbn_sum_acts"])
 def test_nbn_sums_in_dgrad_match_phases_4_5(name, monkeypatch):
     """The BN backward of a fused raw-input Dense -> BN pair reduced in its consumer's DGRAD epilogue
     (GF_NBNSUM + nbn phase 6, dY never stored) against nbn phases 4 / 5 over the stored bf16 dY: the plan uses
