@@ -5,8 +5,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-STEPS=tests bash scripts/gpu_r4.sh || exit 1
-tail -1 gpurun_out/gputests.log; grep -q " passed" gpurun_out/gputests.log && ! tail -1 gpurun_out/gputests.log | grep -q "failed" || exit 1
+if [ -z "$SKIPTESTS" ]; then
+  STEPS=tests bash scripts/gpu_r4.sh || exit 1
+  tail -1 gpurun_out/gputests.log; grep -q " passed" gpurun_out/gputests.log && ! tail -1 gpurun_out/gputests.log | grep -qE "[0-9]+ failed" || exit 1
+fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
 STEPS=tl,step bash scripts/gpu_r4.sh || exit 1
