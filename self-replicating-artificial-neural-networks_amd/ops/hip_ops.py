@@ -783,7 +783,8 @@ def dgrad_reads_natural(KH: int, KW: int, SH: int, SW: int, F: int) -> bool:
     return ("tiled" not in _OFF and "bt" not in _OFF and KH * KW == 1 and SH * SW == 1 and F > BK)
 
 
-SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "32"))   # target k steps per split (0: off; round 2: 48)
+# target k steps per split (0: off; round 2: 48, round 3: 32; 24 from the round-4 sweep, profiles/r4/ab_split_targets.txt)
+SPLIT_KSTEPS = int(_os.environ.get("SERANN_SPLIT_KSTEPS", "24"))
 
 
 def tiled_fwd_splits(M: int, N: int, K: int, bn: int, flags: int) -> int:
@@ -819,7 +820,7 @@ def wgrad_row_groups(M: int, N: int, K: int, bm: int, bn: int) -> int:
 
 
 def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64, rg: int = 1) -> int:
-    """k-steps (32 rows) per WGRAD block: SERANN_WGRAD_TARGET (128), halved (down to 16) while the
+    """k-steps (32 rows) per WGRAD block: SERANN_WGRAD_TARGET (64), halved (down to 16) while the
     problem alone has fewer than WGRAD_MIN_BLOCKS blocks -- a small weight matrix over many rows
     (measured: two [70 x 98] Dense WGRADs over 75000 rows in 57 blocks ran at 0.2 TB/s) splits its
     reduction finer.  A function of the problem alone: the m-split boundaries decide the fp32 partial
@@ -832,7 +833,9 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64, rg: int
     return tg
 
 
-_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "128"))
+# target k steps per WGRAD split (rounds 2-3: 128; 64 from the round-4 sweep: generation-3 mix 17.5 -> 17.0 ms per
+# step on one stream, ancestor neutral, profiles/r4/ab_split_targets.txt)
+_WGRAD_TARGET = int(_os.environ.get("SERANN_WGRAD_TARGET", "64"))
 # whole-F WGRAD tiles (BMF 96..192 x 64 columns) for Dense problems with F in (64, 192] and a short reduction
 # (<= WGRAD_WIDE_MAXK 32-row k steps: the batch-750 Dense layers, single split -> plain store / fused Adam)
 WGRAD_WIDE = _os.environ.get("SERANN_WGRAD_WIDE", "0") != "0"
