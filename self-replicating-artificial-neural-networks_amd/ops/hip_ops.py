@@ -120,13 +120,18 @@ NBN_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "dy", "gamma", "b
 # the multiple of it taken by the reduction phases 4 / 5
 NBN_ELEMS = int(_os.environ.get("SERANN_NBN_ELEMS", "16384"))
 NBN_RED_MULT = int(_os.environ.get("SERANN_NBN_RED_MULT", "4"))
+# phase 2 alone (no reduction, so its block boundaries do not touch the numerics): 131072 elements per block
+# repeat its per-channel prologue 8x less often; ancestor step 5.40 -> 5.20 ms on one stream, 5.54 -> 5.40 at
+# 4 stream groups, generation-3 mix neutral (profiles/r4/ab_nbn_phase2_elems.txt)
+NBN_P2_ELEMS = int(_os.environ.get("SERANN_NBN_P2_ELEMS", "131072"))
 
 
 def nbn_super_rows(units: int, phase: int) -> int:
     """Super-rows (8 rows) per nbn block: a function of the problem alone (the phase 4 / 5 block partial
     sums meet in fixed point, so their boundaries fix the rounding)."""
-    s1 = max(1, (NBN_ELEMS // 8) // int(units))
-    return s1 if phase == 2 else s1 * NBN_RED_MULT
+    if phase == 2:
+        return max(1, (NBN_P2_ELEMS // 8) // int(units))
+    return max(1, (NBN_ELEMS // 8) // int(units)) * NBN_RED_MULT
 
 
 def nbn_chunks(rows: int, units: int, phase: int) -> int:

@@ -163,7 +163,7 @@ def test_nbn_chunking_covers_rows():
     for rows, f in ((75000, 75), (588000, 24), (750 * 100, 200), (17, 8)):
         for phase in (2, 4, 5):
             s1 = max(1, (H.NBN_ELEMS // 8) // f)
-            srb = s1 if phase == 2 else s1 * H.NBN_RED_MULT
+            srb = max(1, (H.NBN_P2_ELEMS // 8) // f) if phase == 2 else s1 * H.NBN_RED_MULT
             assert H.nbn_chunks(rows, f, phase) * srb * 8 >= rows > (H.nbn_chunks(rows, f, phase) - 1) * srb * 8
 
 
