@@ -93,7 +93,8 @@ def supervise(cmd_for, argv: List[str], max_restarts: int, env: Optional[dict] =
     env[CHILD_ENV] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     from ..utils.faults import EXIT_TIMEOUT
-    timed_out_at = None
+    no_timeout = object()                    # sentinel: None is a real value of ``committed`` (nothing committed yet)
+    timed_out_at = no_timeout
     try:
         attempt = 0
         while True:
@@ -111,7 +112,7 @@ def supervise(cmd_for, argv: List[str], max_restarts: int, env: Optional[dict] =
                       file=sys.stderr, flush=True)
                 return rc
             if rc == EXIT_TIMEOUT:
-                if timed_out_at is not None and timed_out_at == committed:
+                if timed_out_at is not no_timeout and timed_out_at == committed:
                     print(f"[launch] the generation watchdog fired again after committed generation {committed}; "
                           f"the same work would time out again: not restarting", file=sys.stderr, flush=True)
                     return rc

@@ -314,9 +314,6 @@ void g3_direct_kernel(const GemmDesc* __restrict__ descs,
     const G3 g = geo3(d);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r16 = lane & 15, kg = (lane >> 4) * 8;
-    // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
-    auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
-    const int kfa = kswz(r16, lane >> 4);
     const int m_w = td.y * BMB + (KW ? 0 : wave * WROWS);
     const int n0 = td.z * BNB;
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
@@ -908,9 +905,6 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     const Div dCp = mkdiv(d.dvCp);
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int r16 = lane & 15, kg = (lane >> 4) * 8;
-    // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
-    auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
-    const int kfa = kswz(r16, lane >> 4);
     const int ohw = g.OH * g.OW;
     const int b = td.y, m0 = td.z, n0 = td.w * BN;
     const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
@@ -2329,9 +2323,10 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         // GF_NBNSUM: the BN-backward-sums epilogue (17000 + BN: transposed weights, 18000 + BN: natural)
 #define TLS(BN_)                                                                                                \
     if (variant == 17000 + BN_) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_, false, true>), grid, block, 0, s, dp, tp); \
-    else if (variant == 18000 + BN_) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_, true, true>), grid, block, 0, s, dp, tp);
+    else if (variant == 18000 + BN_) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, BN_, true, true>), grid, block, 0, s, dp, tp); else
         TLS(64) TLS(128) TLS(160) TLS(192)
 #undef TLS
+        throw std::runtime_error("gemm3: unknown NBNSUM DGRAD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
         return;
     }

@@ -1612,6 +1612,7 @@ class HipPopulationEngine(PopulationEngine):
                 finally:
                     self._bg.stream_only = False
             bg["thread"] = threading.Thread(target=work, name="serann-plan-build", daemon=True)
+            self._plan_thread = bg["thread"]                  # close() joins it if fit() is left early
             bg["thread"].start()
 
         def join_rest():
@@ -1665,6 +1666,28 @@ class HipPopulationEngine(PopulationEngine):
         val_acc = np.full(P, np.nan)
         val_mse = np.full(P, np.nan)
         total = 0
+        try:
+            train_acc, val_acc, val_mse, total, graph = self._fit_epochs(
+                cfg, split, n, steps, full_steps, use_graph, perm_t, counter, metrics, dd, step, remainder_step,
+                start_rest, join_rest, rem, train_acc, val_acc, val_mse, total, graph)
+        finally:
+            if bg["thread"] is not None:                   # left early (HIP error, interrupt): never leave the
+                bg["thread"].join()                        # builder thread allocating behind our back
+                bg["thread"] = None
+        torch.cuda.synchronize(dev)
+        self._train_mem = mem
+        self.graph = graph
+        # every buffer the captured graph addresses lives as long as the graph does
+        self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem["plans"])
+        return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
+                         extra={"plan_s": self.timings["plan_s"], "alloc_s": self.timings["alloc_s"],
+                                "launches_per_step": self.timings["launches_per_step"]})
+
+    def _fit_epochs(self, cfg, split, n, steps, full_steps, use_graph, perm_t, counter, metrics, dd, step,
+                    remainder_step, start_rest, join_rest, rem, train_acc, val_acc, val_mse, total, graph):
+        """The epoch loop of :meth:`fit`: capture on the first full step, replay the rest, remainder step,
+        validation.  Returns (train_acc, val_acc, val_mse, steps run, graph)."""
+        dev = self.device
         for epoch in range(cfg.epochs):
             perm = epoch_permutation(cfg.seed, epoch, split).astype(np.int32)
             perm_t.copy_(torch.from_numpy(perm))
@@ -1709,14 +1732,7 @@ class HipPopulationEngine(PopulationEngine):
             train_acc = m[:, 1] / np.maximum(m[:, 3], 1)
             if cfg.val_every_epoch or epoch == cfg.epochs - 1:
                 val_acc, val_mse = self._evaluate_rows(dd["train_x"], dd["train_g"], dd["train_y"], split, n, cfg)
-        torch.cuda.synchronize(dev)
-        self._train_mem = mem
-        self.graph = graph
-        # every buffer the captured graph addresses lives as long as the graph does
-        self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem["plans"])
-        return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
-                         extra={"plan_s": self.timings["plan_s"], "alloc_s": self.timings["alloc_s"],
-                                "launches_per_step": self.timings["launches_per_step"]})
+        return train_acc, val_acc, val_mse, total, graph
 
     # ---------------------------------------------------------------------------------------------
     def export_arena(self, i: int, arena: torch.Tensor) -> Dict[int, Dict[str, np.ndarray]]:
@@ -1897,6 +1913,10 @@ class HipPopulationEngine(PopulationEngine):
         """Release every device resource the engine owns besides its parameters: the captured graph first
         (its replay addresses the buffers below), then plans, activation / gradient buffers, descriptor
         tables and side streams.  Waits for the device first, so nothing in flight still reads them."""
+        th = getattr(self, "_plan_thread", None)
+        if th is not None:                      # a plan-builder thread of an interrupted fit() still running
+            th.join()
+            self._plan_thread = None
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         self.graph = None

@@ -211,6 +211,35 @@ def test_watchdog_scales_with_shard_and_is_off_for_cpu_runs(monkeypatch):
     W.engine_name = "hip"
     e = Experiment("x", None, W(), None, {"genotype_size": 8, "num_classification_classes": 10}, None)
     assert e._watchdog.timeout_s > 0
+    # a CPU run under the supervising launcher (--max-restarts / --nproc) arms the reference's job timeout
+    W.engine_name = "torch"
+    monkeypatch.setenv(CHILD_ENV, "1")
+    e = Experiment("x", None, W(), None, {"genotype_size": 8, "num_classification_classes": 10}, None)
+    from serann.config import experiment_config
+    assert e._watchdog.timeout_s == float(experiment_config["worker_pool_job_timeout"])
+
+
+def test_supervisor_gives_up_on_repeated_timeout_before_any_commit(tmp_path):
+    """Two watchdog timeouts with nothing committed (committed generation None both times): the same work
+    would time out again, so the supervisor stops after one relaunch instead of using every restart."""
+    import sys
+    import textwrap
+    from serann.cli.launch import supervise
+    from serann.utils.faults import EXIT_TIMEOUT
+    log = tmp_path / "runs.log"
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {repr(str(__import__('pathlib').Path(__file__).resolve().parents[1]))})
+        from serann.cli.launch import record_run_id
+        with open({repr(str(log))}, "a") as f:
+            f.write("run ")
+        record_run_id("exp-1", None)
+        sys.exit({EXIT_TIMEOUT})
+    """))
+    rc = supervise(lambda a: [sys.executable, str(child), *a], [], max_restarts=5)
+    assert rc == EXIT_TIMEOUT
+    assert log.read_text().split() == ["run", "run"]
 
 
 def test_collective_timeout_follows_job_timeout(monkeypatch):
