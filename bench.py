@@ -53,6 +53,17 @@ def main():
     from serann.utils.db import ExperimentDB
 
     comm = make_comm()
+    # the driver's contract: one rank per GPU of one node.  Fail fast on a launch that does not match --gpus
+    # or ranks that share / miss their GPU, instead of timing a different configuration
+    if comm.world_size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {comm.world_size}: launch one rank per GPU")
+    if torch.cuda.is_available() and args.engine in ("auto", "hip"):
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.current_device() != local_rank:
+            raise SystemExit(f"bench.py: rank {comm.rank} computes on cuda:{torch.cuda.current_device()}, "
+                             f"not its LOCAL_RANK {local_rank}")
+        if torch.cuda.device_count() < args.gpus and comm.world_size > 1:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} visible GPUs")
     params = load_parameters(args.parameters) if args.parameters else default_parameters("full_experiment")
     pop = args.pop_per_gpu * comm.world_size
     params["num_seranns"] = pop
@@ -115,6 +126,8 @@ def main():
                                 "architectures from the reference generator distribution)",
                        "global_batch": int(params["training_batch_size"]), "seq_len": int(params["genotype_size"]),
                        "population": pop, "parallelism": f"population-sharded dp{comm.world_size}"},
+            # per generation: "ranks" (GPU index, organisms, predicted / measured learning seconds and shard
+            # wall time of every rank), "allgather_s" / "allgather_bytes" (the one collective per generation)
             "generations": timed,
             # work normalisation: the evolved population (and so the work of a generation) depends on the
             # seeded trajectory; model FLOPs of training per generation and the rate achieved on them

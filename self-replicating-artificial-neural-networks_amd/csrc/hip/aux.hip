@@ -871,6 +871,74 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const SplitFinDesc
     }
 }
 
+// Split WGRAD finalize (serann_hip.h WgFinDesc).  Grouped: tiles (problem, chunk of WGFIN_ELEMS outputs).
+// A block sums 64 outputs over all S splits: the 4 waves take splits w, w + 4, ... (a wave's 64 lanes read 64
+// consecutive slab floats per split, 4 splits in flight), then wave 0 adds the 4 partial sums in wave order --
+// a fixed association, so the result is bitwise reproducible.  (One thread per output walking all S splits
+// left a 15-block launch latency-bound: 100-240 us for a 15 MB slab set.)
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs,
+                                                             const int2* __restrict__ tiles) {
+    __shared__ float part[4][64];
+    const int2 td = tiles[blockIdx.x];
+    const WgFinDesc& d = descs[td.x];
+    const int N = (int)d.N, C = (int)d.C, Cp = (int)d.Cp, S = (int)d.S;
+    const int64_t ldp = (int64_t)(N / C) * Cp;
+    const int64_t slab = d.M * ldp;
+    const int64_t MN = d.M * (int64_t)N;
+    const float* __restrict__ ws = reinterpret_cast<const float*>(d.ws);
+    long long* __restrict__ out = reinterpret_cast<long long*>(d.out);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t e = (int64_t)td.y * WGFIN_ELEMS + lane;
+    const bool ok = e < MN;
+    int64_t src = 0;
+    if (ok) {
+        const int64_t f = e / N;
+        const int col = (int)(e - f * N);
+        const int tap = col / C;
+        src = f * ldp + (int64_t)tap * Cp + (col - tap * C);
+    }
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;     // splits w + 16 i + {0, 4, 8, 12}: 4 loads in flight
+    int s_ = w;
+    if (ok) {
+        for (; s_ + 12 < S; s_ += 16) {
+            const float a = ws[s_ * slab + src], b = ws[(s_ + 4) * slab + src];
+            const float c = ws[(s_ + 8) * slab + src], g = ws[(s_ + 12) * slab + src];
+            v0 += a; v1 += b; v2 += c; v3 += g;
+        }
+        for (; s_ < S; s_ += 4) v0 += ws[s_ * slab + src];
+    }
+    part[w][lane] = (v0 + v1) + (v2 + v3);
+    __syncthreads();
+    if (w != 0 || !ok) return;
+    const float v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    const long long q = fx_q(v);
+    if (d.ldo) {                                      // a column slice of a wider dW (fused-concat K slice)
+        const int64_t f = e / N;
+        out += f * (d.ldo - N);                       // (element e of the slice -> f * ldo + col)
+    }
+    const AdamCtx* ac = reinterpret_cast<const AdamCtx*>(d.adam);
+    if (ac == nullptr) {
+        out[e] = q;
+    } else {
+        // sole writer of this parameter: the optimizer step here (as the GF_ADAM WGRAD epilogue)
+        const int64_t pe = (out - reinterpret_cast<const long long*>(ac->g)) + e;
+        float* P = reinterpret_cast<float*>(ac->p);
+        float* Mo = reinterpret_cast<float*>(ac->m);
+        float* Vo = reinterpret_cast<float*>(ac->v);
+        float p_ = P[pe], m_ = Mo[pe], v_ = Vo[pe];
+        adam_elem(p_, m_, v_, fx_f(q), *reinterpret_cast<const float*>(ac->lr_t), ac->b1, ac->b2, ac->eps);
+        P[pe] = p_; Mo[pe] = m_; Vo[pe] = v_;
+        reinterpret_cast<bf16_t*>(ac->pbf)[pe] = f2bf(p_);
+    }
+}
+
+void launch_wgrad_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),
+                       as_ptr<const WgFinDesc>(descs), as_ptr<const int2>(tiles));
+    SERANN_CHECK(hipGetLastError());
+}
+
 void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
     hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)ntiles), dim3(256), 0, as_stream(stream),

@@ -173,17 +173,29 @@ __device__ __forceinline__ bf16x8_t tr_frag(const bf16_t* lo_p, const bf16_t* hi
 // quad of blocks) keep distinct 128-B bank windows.  Per-NB masks from an exhaustive search over linear
 // maps of the group bits (padding rows to 72 / 136 elements, as before, left 2-way conflicts).
 template <int NB>
-__device__ __forceinline__ int tr_swz(int row, int col) {
-    const int L = row * NB + (col >> 4), G = L >> 3;
-    int h;
-    if constexpr (NB == 1) h = (G & 1) << 2;
-    else if constexpr (NB == 2 || NB == 6 || NB == 10) h = (G >> 1) & 1;
-    else if constexpr (NB == 4 || NB == 12) h = (G & 1) | ((G >> 1) & 2);
-    else if constexpr (NB == 8) h = (G & 3) | ((G >> 1) & 4);
-    else h = ((G >> 1) & 3) | ((G >> 2) & 4);
+__device__ __forceinline__ int tr_swz_h(int G) {
     static_assert(NB == 1 || NB == 2 || NB == 4 || NB == 6 || NB == 8 || NB == 10 || NB == 12 || NB == 16,
                   "tr_swz: no conflict-free map searched for this row width");
-    return ((L ^ h) << 4) | (col & 15);
+    if constexpr (NB == 1) return (G & 1) << 2;
+    else if constexpr (NB == 2 || NB == 6 || NB == 10) return (G >> 1) & 1;
+    else if constexpr (NB == 4 || NB == 12) return (G & 1) | ((G >> 1) & 2);
+    else if constexpr (NB == 8) return (G & 3) | ((G >> 1) & 4);
+    else return ((G >> 1) & 3) | ((G >> 2) & 4);
+}
+template <int NB>
+__device__ __forceinline__ int tr_swz(int row, int col) {
+    const int L = row * NB + (col >> 4);
+    return ((L ^ tr_swz_h<NB>(L >> 3)) << 4) | (col & 15);
+}
+// The same map as seen by a lane-linear writer (LDS-DMA: lane i of a wave instruction writes 16-B piece q0 + i):
+// physical 16-B piece q holds logical (row, 8-column piece) of block L = P ^ h(P >> 3), P = q >> 1 (the XOR
+// only touches the low 3 bits of the block index, so it is its own inverse within the 256-B group)
+template <int NB>
+__device__ __forceinline__ void tr_swz_piece(int q, int& row, int& col) {
+    const int P = q >> 1;
+    const int L = P ^ tr_swz_h<NB>(P >> 3);
+    row = L / NB;
+    col = (L - row * NB) * 16 + (q & 1) * 8;
 }
 
 // ---- im2col chunk (FWD A operand, WGRAD B operand) -------------------------------------------
@@ -1056,43 +1068,83 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 }
 
 // ==================================================================================================
-// WGRAD of a KHxKW > 1 convolution with the input patch staged in LDS.
-//   dWm[f][tap][c] += sum_m dZ[m][f] * X[patch(m) + tap][c]
-// A block owns an f tile (BMF) x a k' tile (BNK columns of the padded (tap, Cp) reduction space) and
-// sweeps a range of 128-pixel chunks [td.z, td.w) (chunk = (image, pixel tile)).  Per chunk it stages
-// the chunk's input rows (padded channels, as in g3_conv_fwd_kernel) and its 128 dZ rows (act' applied)
-// in LDS; both MFMA operands are then read with ds_read_b64_tr_b16 -- the B operand (im2col) with
-// per-lane addresses into the patch, so every input element is fetched from global once per chunk
-// instead of KH*KW times.  Accumulators stay in registers across chunks; one fp32 atomic flush at the
-// end (the bias gradient is reduced by the k'-tile-0 blocks from the staged dZ rows).
+// WGRAD of a KHxKW > 1 convolution with the input patch staged in LDS, as tap-shifted GEMMs.
+//   dWm[f][tap][c] += sum_m dZ[m][f] * X[patch(m) + shift(tap)][c]
+// A block owns BMF filters x BNK columns of the padded (tap, Cp) reduction space and sweeps a range of
+// 128-pixel chunks [td.z, td.w) (chunk = (image, pixel tile)).  Every wave holds ALL TF = BMF / 16 filter
+// tiles and NTW = BNK / 64 column tiles (columns j*64 + 16*wave of the block).  Per 32-row MFMA k step a
+// wave reads its TF dZ fragments once; its column tiles are then pure LDS base shifts of one per-row patch
+// address: tap (kh, kw) of output pixel m is input pixel patch(m) + kh * W + kw, so a B fragment is two
+// ds_read_b64_tr_b16 at (row address + column offset) -- no per-lane im2col division, no restaging per
+// column tile.  Stride 2 is the same loop (patch(m) carries the stride).
+// Staging is an NST-deep ring of LDS stages filled by LDS-DMA (buffer_load ... lds: no VGPRs, no ds_write):
+// the patch (padded channels: pixel p at p * Cs, an odd number of 16-B slots per pixel; pad slots and pixels
+// past the patch load out of range = zeros), the raw dY tile and the Y tile (act' is applied to the A fragments
+// in registers), and the per-row patch offsets.  Chunk ch + NST - 1 is issued while chunk ch is computed, so
+// NST - 1 chunks of loads are in flight behind the MFMAs (a one-deep register prefetch left the loop waiting
+// on load latency: ~3.5 us per chunk against ~0.5 us of MFMAs on a 16-filter problem).  Every DMA count is
+// fixed per chunk, so the ring is retired with counted vmcnt waits and raw s_barriers (a __syncthreads would
+// drain every DMA in flight).  Accumulators stay in registers across chunks; the flush writes fp32 split slabs
+// (or the Q32 gradient of a single split); the bias gradient is reduced from the dZ fragments by wave 0 of
+// the blocks of column range 0.
 // Small outputs (OH*OW < 128, e.g. a 7x7 conv on an 11x11 map: 25 pixels) would leave most of a
 // 128-row chunk empty, so a chunk then covers ipc = min(128 / (OH*OW), PATCH / (H*W*Cs)) whole
 // consecutive images when ipc >= 2 (their input images are one contiguous NHWC range; hip_ops
 // conv_wgrad_ipc mirrors the rule for the tile table).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only (gfx9 encoding; expcnt / lgkmcnt max)
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// LDS-DMA stages of the conv WGRAD ring: 3 when two blocks of them fit a CU's 160 KB (latency hidden by two blocks
+// and two chunks in flight each), else as many as one block can hold (at most 4, at least 2)
+constexpr int conv_wgrad_stages(int stage_bytes) {
+    return 3 * stage_bytes <= 80 * 1024 ? 3
+           : (4 * stage_bytes <= 160 * 1024 ? 4 : (3 * stage_bytes <= 160 * 1024 ? 3 : 2));
+}
 template <int BMF, int BNK, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
-    constexpr int TM = 128, LDA = BMF, NBA = BMF / 16;   // dZ tile: unpadded rows, tr_swz blocks
-    // patch + one 16-B dump slot for the staging writes of pieces past the chunk's patch
-    __shared__ __attribute__((aligned(16))) bf16_t patch[PATCH + 8];
-    __shared__ __attribute__((aligned(16))) bf16_t As[TM * LDA];
-    __shared__ int rtab[TM];              // per chunk row: patch element offset of its receptive field
+    constexpr int TM = 128, NBA = BMF / 16;
+    constexpr int TF = BMF / 16, NTW = BNK / 64;
+    static_assert(BNK % 256 == 0 || BNK == 128, "column tiles: NTW in {2, 4, 8, 16, 32}");
+    constexpr int DYT = TM * BMF;                         // bf16 elements of the dY (and of the Y) tile
+    constexpr int STG = PATCH + 2 * DYT + 2 * TM;         // stage: patch, dY, Y, row offsets (TM ints)
+    constexpr int NST = conv_wgrad_stages(STG * 2);
+    static_assert(NST * STG * 2 <= 160 * 1024, "conv WGRAD stages exceed the LDS");
+    constexpr int PD = PATCH / 2048;                      // patch DMAs per thread and chunk (16-B pieces / 256)
+    constexpr int AD = DYT / 2048;                        // dY DMAs per thread and chunk (as many Y DMAs)
+    constexpr int PER = PD + 2 * AD;                      // vector-memory ops per thread and chunk (fixed)
+    // ONE shared array (a second __shared__ object beside LDS-DMA targets makes hipcc drain vmcnt before reads)
+    __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STG];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
     const Div dCp = mkdiv(d.dvCp);
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // (the wave index through readfirstlane: wave-uniform in an SGPR, so per-wave values are scalar)
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int f0 = (td.y >> 16) * BMF, kc0 = (td.y & 0xffff) * BNK;
     const int ohw = g.OH * g.OW;
     const int tpi = (ohw + TM - 1) / TM;
     const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
-    const int Cs = (C8 & 1) ? Cp : Cp + 8;
+    const int Cs = (C8 & 1) ? Cp : Cp + 8, Cs8 = Cs >> 3;
+    // q / Cs8 for slot indices q < 2^12 (PATCH / 8): (q * mCs) >> 17, mCs = ceil(2^17 / Cs8), exact for Cs8 <= 32;
+    // wider channels use the generic magic (fdiv)
+    const uint32_t mCs = (131072u + Cs8 - 1) / (uint32_t)Cs8;
+    const bool small_cs = Cs8 <= 32;
+    Div dCs8;
+    {
+        const uint32_t dv = (uint32_t)Cs8;
+        uint32_t sh = 0;
+        while ((1u << sh) < dv) ++sh;
+        dCs8.mul = (uint32_t)(((1ull << 32) * ((1ull << sh) - dv)) / dv + 1);
+        dCs8.sh = sh;
+    }
     const int taps = g.KH * g.KW;
     const int nbatch = g.K / ohw;
     const int hwcs = g.H * g.W * Cs;
     const int ipc_full = ohw < TM ? min(TM / ohw, PATCH / hwcs) : 0;
     const bool multi = ipc_full >= 2;            // chunk = ipc whole images
-    // chunk -> (first image, first pixel, last pixel of the chunk relative to that image's pixel 0)
     auto chunk_geom = [&](int ch, int& b, int& m0, int& m_last) {
         if (multi) {
             b = ch * ipc_full;
@@ -1108,22 +1160,16 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
     long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
-    const uint4 zero = make_uint4(0, 0, 0, 0);
-
-    constexpr int WR = (BMF == 64) ? 2 : 1;          // waves along f
-    constexpr int WC = 4 / WR;                       // waves along k'
-    constexpr int TF = BMF / WR / 16;
-    constexpr int TK = BNK / WC / 16;
-    const int wf = wave / WC, wk = wave % WC;
     const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const bool has_act = g.act != ACT_LINEAR;
 
-    // per-lane im2col column offsets: column k' = kc0 + wk*(BNK/WC) + j*16 + 4*pp (4 consecutive
-    // channels of one tap).  Columns past the reduction read a valid patch address (zero B is not
-    // needed: their accumulators are never stored).
-    int coff[TK];
+    // column tiles of this wave: block column kc0 + (j * 4 + wave) * 16; valid ones first, nvj of them
+    const int ncolt = min(4 * NTW, (taps * Cp - kc0 + 15) >> 4);
+    const int nvj = ncolt > wave ? (ncolt - wave + 3) >> 2 : 0;
+    int coff[NTW];
 #pragma unroll
-    for (int j = 0; j < TK; ++j) {
-        const int kp = kc0 + wk * (BNK / WC) + j * 16 + 4 * pp;
+    for (int j = 0; j < NTW; ++j) {
+        const int kp = kc0 + (j * 4 + wave) * 16 + 4 * pp;
         int tap = fdiv(kp, dCp);
         const int c = kp - tap * Cp;
         tap = min(tap, taps - 1);
@@ -1131,158 +1177,185 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         const int kw = tap - kh * g.KW;
         coff[j] = (kh * g.W + kw) * Cs + c;
     }
-
-    // dZ loader: rows m (TM) x f (BMF) in chunks of 8 f
-    constexpr int ACH = BMF / 8;
-    const int a_f = (t % ACH) * 8, a_r0 = t / ACH;
-    constexpr int AROWS = 256 / ACH;
-    const int a_nv = min(8, g.F - (f0 + a_f));
-    const bool do_bias = dbias != nullptr && kc0 == 0;
-    float bsum[8];
+    const bool do_bias = dbias != nullptr && kc0 == 0 && wave == 0;
+    float bsum[TF];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-
-    f32x4_t acc[TF][TK];
+    for (int i = 0; i < TF; ++i) bsum[i] = 0.f;
+    f32x4_t acc[TF][NTW];
 #pragma unroll
     for (int i = 0; i < TF; ++i)
 #pragma unroll
-        for (int j = 0; j < TK; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // Software pipeline over chunks: the global loads of chunk ch+1 (patch and dZ rows) are issued
-    // into registers before the MFMAs of chunk ch and land in LDS after them, so their latency hides
-    // behind compute (one LDS copy of each operand; two barriers per chunk).
-    constexpr int PLD = PATCH / 2048;               // 16-B patch pieces per thread (max)
-    constexpr int ALD = (TM * ACH + 255) / 256;     // 16-B dZ pieces per thread
-    uint4 pre[PLD], apre[ALD], ypre[ALD];
-    int cur_npix = 0;
-    auto fetch = [&](int ch) {
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    // Issue every load of chunk ch into stage st: exactly PER buffer_load ... lds per thread (pieces past the
+    // patch / tile load out of range: zeros), and the stage's row offsets (ds_write, ordered by the barrier
+    // that precedes the stage's use).
+    auto issue = [&](int ch, int st) {
         int b, m0, m_last;
         chunk_geom(ch, b, m0, m_last);
-        int npix, gbase;
+        int npix, gbase, oh_a = 0;
         if (multi) {
             npix = (m_last / ohw + 1) * g.H * g.W;       // whole images
             gbase = b * g.H * g.W * g.C;
         } else {
-            const int oh_a = fdiv(m0, g.dOW);
+            oh_a = fdiv(m0, g.dOW);
             const int oh_b = fdiv(m_last, g.dOW);
             npix = ((oh_b - oh_a) * g.SH + g.KH) * g.W;
             gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
         }
-        cur_npix = npix;
+        bf16_t* const stage = smem + st * STG;
 #pragma unroll
-        for (int k = 0; k < PLD; ++k) {
-            const int u = t + k * 256;
-            const int p = fdiv(u * 8, dCp);
-            const int c = u * 8 - p * Cp;
-            pre[k] = bl16(rX, p < npix ? gbase + p * g.C + c : -1);
+        for (int k = 0; k < PD; ++k) {
+            const int q0 = (k * 4 + wave) * 64;          // wave-uniform first slot of this instruction
+            const int qq = q0 + lane;
+            const int p = small_cs ? (int)(((uint32_t)qq * mCs) >> 17) : fdiv(qq, dCs8);
+            const int c8 = qq - p * Cs8;
+            const int off = (p < npix && c8 < C8) ? (gbase + p * g.C + c8 * 8) * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_ptr_t)(stage + q0 * 8), 16, off, 0, 0, 0);
         }
-        // C % 8 != 0: the pad channels of a pixel hold the next pixel's first channels.  They are left
-        // as they are: a pad channel only feeds the accumulator columns (tap, c >= C), which the flush
-        // never stores (zeroing them per piece kept ~60 loop-invariant lane masks live: SGPR spills)
+        bf16_t* const dyt = stage + PATCH;
 #pragma unroll
-        for (int k = 0; k < ALD; ++k) {
-            const int r = a_r0 + k * AROWS;
+        for (int k = 0; k < AD; ++k) {
+            const int q0 = (k * 4 + wave) * 64;
+            int r, fc;
+            tr_swz_piece<NBA>(q0 + lane, r, fc);        // the logical piece the swizzled reads expect here
             const int m = m0 + r;
-            const bool ok = r < TM && a_nv > 0 && m <= m_last;
-            const int off = ok ? (b * ohw + m) * g.F + f0 + a_f : -1;
-            apre[k] = bl16(rZ, off);                  // raw: act' is applied when staged (as in
-            if (g.act != ACT_LINEAR) ypre[k] = bl16(rY, off);   // g3_wgrad_kernel)
-        }
-    };
-
-    if (td.z < td.w) fetch(td.z);
-    for (int ch = td.z; ch < td.w; ++ch) {
-        int b, m0, m_last;
-        chunk_geom(ch, b, m0, m_last);
-        const int oh_a = multi ? 0 : fdiv(m0, g.dOW);
-        const int npix = cur_npix;
-        __syncthreads();                              // previous chunk's LDS reads are done
-#pragma unroll
-        for (int k = 0; k < PLD; ++k) {
-            const int u = t + k * 256;
-            const int p = fdiv(u * 8, dCp);
-            const int c = u * 8 - p * Cp;
-            *reinterpret_cast<uint4*>(&patch[p < npix ? p * Cs + c : PATCH]) = pre[k];
+            const int off = (m <= m_last && f0 + fc < g.F) ? ((b * ohw + m) * g.F + f0 + fc) * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rZ, (lds_ptr_t)(dyt + q0 * 8), 16, off, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rY, (lds_ptr_t)(dyt + DYT + q0 * 8), 16, has_act ? off : OOB,
+                                                     0, 0, 0);
         }
         if (t < TM) {
-            // row offsets, once per chunk (the MFMA loop reads them instead of redoing the
-            // pixel -> (image, oh, ow) divisions per lane, sub-step and row quad); rows past the chunk
-            // end read a valid pixel (their dZ rows are zero)
+            // row offsets (rows past the chunk end read a valid pixel: their dZ rows are zero)
             int m = m0 + t;
             if (m > m_last) m = m0;
             const int j = multi ? fdiv(m, g.dOHW) : 0;     // image inside the chunk
             const int pm = m - j * ohw;
             const int oh = fdiv(pm, g.dOW);
             const int ow = pm - oh * g.OW;
-            rtab[t] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+            reinterpret_cast<int*>(stage + PATCH + 2 * DYT)[t] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
         }
+    };
+
+    const int z = td.z, w = td.w;
 #pragma unroll
-        for (int k = 0; k < ALD; ++k) {
-            const int r = a_r0 + k * AROWS;
-            if (r < TM) {
-                uint4 v = apre[k];
-                if (g.act != ACT_LINEAR) v = mul_act_grad(v, ypre[k], g.act);
-                if (a_nv < 8) v = splice(v, zero, a_nv);
-                *reinterpret_cast<uint4*>(&As[tr_swz<NBA>(r, a_f)]) = v;
-                if (do_bias) {
-                    Frag fv;
-                    fv.u = v;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) bsum[j] += bf2f(fv.h[j]);
-                }
-            }
-        }
-        __syncthreads();
-        if (ch + 1 < td.w) fetch(ch + 1);
+    for (int s_ = 0; s_ < NST - 1; ++s_)
+        if (z + s_ < w) issue(z + s_, s_);
+    int st = 0;
+    for (int ch = z; ch < w; ++ch) {
+        // retire chunk ch's loads: the chunks issued after it (at most NST - 2) stay in flight
+        const int ahead = min(NST - 2, w - 1 - ch);
+        if (NST >= 4 && ahead >= 2) wait_vmcnt<(NST >= 4 ? 2 * PER : 0)>();
+        else if (NST >= 3 && ahead >= 1) wait_vmcnt<(NST >= 3 ? PER : 0)>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // row offsets written
+        __builtin_amdgcn_s_barrier();
+        // the stage of chunk ch - 1 is free now (every wave is past its reads): refill it
+        if (ch + NST - 1 < w) issue(ch + NST - 1, st == 0 ? NST - 1 : st - 1);
+        const bf16_t* const patch = smem + st * STG;
+        const bf16_t* const dyt = patch + PATCH;
+        const bf16_t* const yt = dyt + DYT;
+        const int* const rt = reinterpret_cast<const int*>(yt + DYT);
 #pragma unroll
         for (int sub = 0; sub < TM / 32; ++sub) {
-            // rows of this lane's two tr-read quads
             const int mr = sub * 32 + grp * 8 + q;
-            const bf16_t* p0 = patch + rtab[mr];
-            const bf16_t* p1 = patch + rtab[mr + 4];
-            bf16x8_t fa[TF], fbk[TK];
+            const bf16_t* p0 = patch + rt[mr];
+            const bf16_t* p1 = patch + rt[mr + 4];
+            bf16x8_t fa[TF];
 #pragma unroll
             for (int i = 0; i < TF; ++i) {
-                const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
-                fa[i] = tr_frag(&As[tr_swz<NBA>(mr, col)], &As[tr_swz<NBA>(mr + 4, col)]);
+                const int col = i * 16 + 4 * pp;
+                bf16x8_t v = tr_frag(&dyt[tr_swz<NBA>(mr, col)], &dyt[tr_swz<NBA>(mr + 4, col)]);
+                if (has_act) {
+                    const bf16x8_t y = tr_frag(&yt[tr_swz<NBA>(mr, col)], &yt[tr_swz<NBA>(mr + 4, col)]);
+                    v = __builtin_bit_cast(bf16x8_t, mul_act_grad(__builtin_bit_cast(uint4, v),
+                                                                  __builtin_bit_cast(uint4, y), g.act));
+                }
+                fa[i] = v;
+                if (do_bias) {
+                    Frag fv;
+                    fv.v = v;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[i] += bf2f(fv.h[e]);
+                }
             }
+            // every column tile of the block, branch-free (tiles past the reduction read a valid address; the
+            // flush drops them): the B fragments of group g + 1 (4 tiles) are read while group g's MFMAs run
+            constexpr int JG = NTW < 4 ? NTW : 4, NG = NTW / JG;
+            bf16x8_t fb[2][JG];
 #pragma unroll
-            for (int j = 0; j < TK; ++j) fbk[j] = tr_frag(p0 + coff[j], p1 + coff[j]);
+            for (int jj = 0; jj < JG; ++jj) fb[0][jj] = tr_frag(p0 + coff[jj], p1 + coff[jj]);
 #pragma unroll
-            for (int i = 0; i < TF; ++i)
+            for (int gq = 0; gq < NG; ++gq) {
+                if (gq + 1 < NG) {
 #pragma unroll
-                for (int j = 0; j < TK; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbk[j], acc[i][j], 0, 0, 0);
+                    for (int jj = 0; jj < JG; ++jj) {
+                        const int j = (gq + 1) * JG + jj;
+                        fb[(gq + 1) & 1][jj] = tr_frag(p0 + coff[j], p1 + coff[j]);
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < JG; ++jj)
+#pragma unroll
+                    for (int i = 0; i < TF; ++i)
+                        acc[i][gq * JG + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[gq & 1][jj],
+                                                                                     acc[i][gq * JG + jj], 0, 0, 0);
+            }
         }
+        st = st + 1 == NST ? 0 : st + 1;
     }
 
     if (do_bias) {
+        // lane l holds the 8-row sums of filter l % 16 of each f tile: add the 4 row groups
 #pragma unroll
-        for (int xo = ACH; xo < 64; xo <<= 1)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
-        if (lane < ACH && a_r0 < TM) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
+        for (int i = 0; i < TF; ++i) {
+            bsum[i] += __shfl_xor(bsum[i], 16, 64);
+            bsum[i] += __shfl_xor(bsum[i], 32, 64);
+            const int f = f0 + i * 16 + lane;
+            if (lane < 16 && f < g.F) fx_add(dbias + f, bsum[i]);
         }
     }
-    // flush: column k' -> (tap, c) -> dWm[f][tap*C + c] for c < C
+    // Flush.  Split problems (d.ext = fp32 slab workspace [S][M][taps * Cp], split = td.z / d.kper): plain
+    // stores of the block's partial tile in the padded column space; the grouped wgrad_finalize launch adds
+    // the splits in order (no fixed-point atomics: at 16 x 1024 columns per block they were ~30x the MFMA
+    // time).  A single split (GF_WSTORE) stores the Q32 gradient dWm[f][tap * C + c] itself.
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
-    long long* out = reinterpret_cast<long long*>(d.out);
+    if (d.ext) {
+        const int ldp = taps * Cp;
+        float* __restrict__ slab = reinterpret_cast<float*>(d.ext) + (int64_t)(td.z / (int)d.kper) * g.M * ldp;
 #pragma unroll
-    for (int j = 0; j < TK; ++j) {
-        const int kp = kc0 + wk * (BNK / WC) + j * 16 + c16;
+        for (int j = 0; j < NTW; ++j) {
+            const int kp = kc0 + (j * 4 + wave) * 16 + c16;
+            if (j >= nvj || kp >= ldp) continue;
+#pragma unroll
+            for (int i = 0; i < TF; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = f0 + i * 16 + rq + r;
+                    if (row < g.M) slab[(int64_t)row * ldp + kp] = acc[i][j][r];
+                }
+        }
+        return;
+    }
+    long long* out = reinterpret_cast<long long*>(d.out);
+    const bool sole = g.flags & GF_WSTORE;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+        const int kp = kc0 + (j * 4 + wave) * 16 + c16;
         const int tap = fdiv(kp, dCp);
         const int c = kp - tap * Cp;
-        if (tap >= taps || c >= g.C) continue;
+        if (j >= nvj || tap >= taps || c >= g.C) continue;
         const int col = tap * g.C + c;
 #pragma unroll
         for (int i = 0; i < TF; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row < g.M) fx_add(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                const int row = f0 + i * 16 + rq + r;
+                if (row < g.M) {
+                    if (sole) out[(int64_t)row * g.N + col] = fx_q(acc[i][j][r]);
+                    else fx_add(out + (int64_t)row * g.N + col, acc[i][j][r]);
+                }
             }
     }
 }
@@ -2239,7 +2312,8 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 // variant encoding (WGRAD): BMF * 1000 + BNK (+ 1000000 * GEN); BMF in {16, 32, 64}, BNK in {16, 64, 128, 256}
 //                 narrow (K <= 4): 4000000 + K (+ 100: LDS-staged rows, + 200: super-row form; F % 8 != 0);
 //                 tiles (prob, row block, 0, 0)
-//                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK (BNK 128/256/512);
+//                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK / 64 (column tiles per wave:
+//                 2 .. 32);
 //                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
 void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
@@ -2263,13 +2337,17 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         const int tier = (variant / 100000) % 10;
         const int v = variant % 100000;
 #define CW3T(BMF_, BNK_, TIER_, PATCH_)                                                               \
-    if (v == BMF_ * 1000 + BNK_ && tier == TIER_) {                                                   \
+    if (v == BMF_ * 1000 + BNK_ / 64 && tier == TIER_) {                                                   \
         hipLaunchKernelGGL((g3_conv_wgrad_kernel<BMF_, BNK_, PATCH_>), grid, block, 0, s, dp, tp);     \
         SERANN_CHECK(hipGetLastError());                                                              \
         return;                                                                                       \
     }
 #define CW3(BMF_, BNK_) CW3T(BMF_, BNK_, 0, 8192) CW3T(BMF_, BNK_, 1, 16384) CW3T(BMF_, BNK_, 2, 32768)
-        CW3(16, 512) CW3(16, 256) CW3(16, 128) CW3(32, 512) CW3(32, 256) CW3(32, 128) CW3(64, 256) CW3(64, 128)
+        // (the 64 KB patch tier is instantiated for 16-filter blocks only: two stages of it fill the LDS)
+#define CW3S(BMF_, BNK_) CW3T(BMF_, BNK_, 0, 8192) CW3T(BMF_, BNK_, 1, 16384)
+        CW3(16, 2048) CW3(16, 1024) CW3(16, 512) CW3(16, 256) CW3(16, 128)
+        CW3S(32, 1024) CW3S(32, 512) CW3S(32, 256) CW3S(32, 128) CW3S(64, 512) CW3S(64, 256) CW3S(64, 128)
+#undef CW3S
 #undef CW3T
 #undef CW3
         throw std::runtime_error("gemm3: unknown conv WGRAD variant " + std::to_string(variant));

@@ -22,6 +22,7 @@ static py::dict desc_sizes() {
     d["TransDesc"] = sizeof(TransDesc);
     d["ImcolDesc"] = sizeof(ImcolDesc);
     d["SplitFinDesc"] = sizeof(SplitFinDesc);
+    d["WgFinDesc"] = sizeof(WgFinDesc);
     d["ConvPoolDesc"] = sizeof(ConvPoolDesc);
     d["GChainDesc"] = sizeof(GChainDesc);
     d["RepBitsDesc"] = sizeof(RepBitsDesc);
@@ -56,6 +57,7 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("imcol", &launch_imcol);
     m.def("embed_gather", &launch_embed_gather);
     m.def("splitk_finalize", &launch_splitk_finalize);
+    m.def("wgrad_finalize", &launch_wgrad_finalize);
     m.def("rep_bits", &launch_rep_bits);
     m.def("concrete_fwd", &launch_concrete_fwd);
     m.def("concrete_bwd", &launch_concrete_bwd);

@@ -77,6 +77,14 @@ void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int6
 void launch_cat_loglik_bwd(uint64_t z, uint64_t x, uint64_t gout, uint64_t dz, int64_t B, int64_t L, int64_t V,
                            uint64_t stream);
 void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
+// Split WGRAD finalize (aux.hip): a WGRAD problem split over S row ranges leaves one fp32 slab per split,
+// ws[S][M][ldp] with ldp = (N / C) * Cp (the kernel's padded (tap, Cp) columns; Cp = C for Dense), written
+// with plain stores; the finalize adds the S slabs IN SPLIT ORDER (bitwise reproducible, no atomics) and
+// stores the Q32 gradient out[M][N] (N = taps * C) -- or, with adam != 0, applies Keras-Adam to those
+// parameters (the gradient quantised as the Q32 arena would hold it; the arena-wide Adam pass skips them).
+struct WgFinDesc { int64_t ws, out, adam, M, N, C, Cp, S, ldo, flags; };   // ldo: out row stride (0: N)
+constexpr int WGFIN_ELEMS = 64;       // outputs per block
+void launch_wgrad_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_embed_gather(uint64_t tokens, uint64_t table, uint64_t out, int64_t rows, int64_t E, int64_t V,
                          uint64_t stream);
 void launch_group_argmax(uint64_t logits, uint64_t out, int64_t ngroups, int64_t V, uint64_t stream);

@@ -32,7 +32,7 @@ import numpy as np
 import pandas as pd
 
 from ..genome.interpreter import layer_counts
-from ..parallel.comm import Comm, LocalComm, pack_header, unpack_results
+from ..parallel.comm import Comm, LocalComm, pack_header, unpack_header, unpack_results
 from ..parallel.partition import RankSpeedModel, lpt_partition
 from ..utils.faults import GenerationWatchdog, job_scale, maybe_inject
 from ..utils.levenshtein import levenshtein_batch
@@ -167,6 +167,9 @@ class Experiment:
             wp = getattr(self._worker, "last_phases", None)
             if wp:
                 record["shard_phases"] = {k: round(v, 4) for k, v in wp.items()}      # this rank's shard
+            record["ranks"] = times.get("ranks", [])
+            record["allgather_s"] = round(float(times.get("allgather_s", 0.0)), 5)
+            record["allgather_bytes"] = int(times.get("allgather_bytes", 0))
             if self._comm.world_size > 1:
                 ms = [v for v in times["rank_measured_s"] if v > 0]
                 record["rank_imbalance"] = max(ms) / (sum(ms) / len(ms)) if ms else float("nan")
@@ -269,15 +272,19 @@ class Experiment:
         ids = list(current.index)
         genotypes = np.stack([np.asarray(g, np.float64) for g in current["genotype"]])
         position = {int(t): k for k, t in enumerate(plan.trainable)}
+        t_shard = time.perf_counter()
         res = self._worker.run(local, [ids[i] for i in local], genotypes[local] if local else genotypes[:0],
                                [plan.results[i].ir for i in local], int(pool_size), generation,
                                self._random_seed, positions=[position[i] for i in local],
                                n_trainable=len(plan.trainable))
-        # one packed all-gather: host header (indices, metrics, timings) + the offspring bits, which stay on
-        # the device from the replication epilogue to the collective (RCCL)
+        t_shard = time.perf_counter() - t_shard
+        # one packed all-gather: host header (indices, metrics, timings, GPU index) + the offspring bits,
+        # which stay on the device from the replication epilogue to the collective (RCCL)
         head = pack_header(res.indices, res.metrics, int(pool_size), int(p["genotype_size"]), res.learning_time,
-                           res.replication_time)
+                           res.replication_time, device=comm.device_index(), shard_s=t_shard)
+        t_ag = time.perf_counter()
         gathered = comm.allgather_payload(head, res.packed)
+        t_ag = time.perf_counter() - t_ag
 
         n = len(current)
         metrics = np.full((n, 4), np.nan)
@@ -296,6 +303,17 @@ class Experiment:
         predicted = [float(sum(plan.costs[j] for j in part)) for part in parts]
         times["rank_predicted_s"], times["rank_measured_s"] = predicted, measured
         times["rank_factors"] = self._speeds.update(predicted, measured)
+        # per-rank load balance and the collective's own cost, for the multi-GPU records (SCALE runs): every
+        # rank's GPU, organisms, predicted (cost model) and measured (learning) seconds and shard wall time
+        ranks = []
+        for r, blob in enumerate(gathered):
+            h = unpack_header(blob)
+            ranks.append(dict(rank=r, device=h["device"], organisms=h["organisms"],
+                              predicted_s=round(predicted[r], 4), measured_s=round(h["learning_s"], 4),
+                              shard_s=round(h["shard_s"], 4)))
+        times["ranks"] = ranks
+        times["allgather_s"] = t_ag
+        times["allgather_bytes"] = int(sum(len(b) for b in gathered))
 
         models_info = pd.DataFrame(index=current.index)
         models_info["parameters_count"] = [r.parameters_count for r in plan.results]

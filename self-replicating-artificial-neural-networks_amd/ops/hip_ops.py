@@ -36,6 +36,8 @@ EW_DTYPE = np.dtype([("a", _I), ("b", _I), ("out", _I), ("D", _I, (4,)), ("R", _
 EW_ELEMS = 2048        # ew.hip: destination elements per block
 SPLITFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "bias", "M", "N", "S", "act", "flags"]])
 SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kernel
+WGFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "adam", "M", "N", "C", "Cp", "S", "ldo", "flags"]])
+WGFIN_ELEMS = 64       # aux.hip: outputs per block of the split WGRAD finalize kernel
 CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy", "dw", "dbias", "B", "H", "W", "F",
                                              "KH", "KW", "SH", "SW", "OH", "OW", "PH", "PW", "PSH", "PSW", "POH",
                                              "POW", "act", "flags"]])
@@ -205,6 +207,49 @@ def adam_skip_mask(n: int, regions) -> np.ndarray:
     return (b[:, 0] | (b[:, 1] << 1) | (b[:, 2] << 2) | (b[:, 3] << 3)).astype(np.uint8)
 
 
+def adam_skip_mask_device(n: int, regions, device):
+    """:func:`adam_skip_mask` built on ``device`` without materialising a per-parameter array on the host
+    (a 100M-parameter shard made that ~0.1 s of numpy per generation).  Every region row is a parameter
+    range [s, e): the 4-parameter groups it covers whole get 0xF (a difference array + cumsum marks them),
+    its at most 3 + 3 edge parameters their own bit.  Regions are disjoint parameter sets, so no bit is set
+    twice and the edge bits add up to their OR."""
+    import torch
+    ng = (int(n) + 3) // 4
+    starts, ends = [], []
+    for off, rows, cols, ld in regions:
+        off, rows, cols, ld = int(off), int(rows), int(cols), int(ld)
+        if rows <= 0 or cols <= 0:
+            continue
+        if ld == cols:
+            starts.append(np.array([off], np.int64))
+            ends.append(np.array([off + rows * cols], np.int64))
+        else:
+            r0 = off + np.arange(rows, dtype=np.int64) * ld
+            starts.append(r0)
+            ends.append(r0 + cols)
+    if not starts:
+        return torch.zeros(ng, dtype=torch.uint8, device=device)
+    s_, e_ = np.concatenate(starts), np.concatenate(ends)
+    ga, gb = (s_ + 3) // 4, e_ // 4                  # whole groups [ga, gb)
+    full = ga < gb
+    idx = np.concatenate([ga[full], gb[full]])
+    val = np.concatenate([np.ones(int(full.sum()), np.int32), -np.ones(int(full.sum()), np.int32)])
+    edge_e = []
+    for k in range(3):
+        e = s_ + k                                   # head: before the first whole group
+        edge_e.append(e[(e < e_) & (e < ga * 4)])
+        e = gb * 4 + k                               # tail: after the last whole group
+        edge_e.append(e[(e >= s_) & (e < e_) & (e >= ga * 4)])
+    ee = np.unique(np.concatenate(edge_e))
+    d = torch.zeros(ng + 1, dtype=torch.int32, device=device)
+    d.index_add_(0, torch.as_tensor(idx, device=device), torch.as_tensor(val, device=device))
+    m = (torch.cumsum(d[:ng], 0) > 0).to(torch.int32) * 15
+    if len(ee):
+        m.index_add_(0, torch.as_tensor(ee // 4, device=device),
+                     torch.as_tensor((1 << (ee % 4)).astype(np.int32), device=device))
+    return m.to(torch.uint8)
+
+
 def bn_chunks(rows: int, channels: int, stats: bool = False) -> int:
     """Blocks of a BatchNorm problem [rows][channels] (aux.hip bn_kernel chunking); ``stats``: a
     statistics phase (0 or 4)."""
@@ -347,6 +392,7 @@ def check_layouts():
     for name, dt in [("GemmDesc", GEMM_DTYPE), ("BnDesc", BN_DTYPE), ("EwDesc", EW_DTYPE),
                      ("PoolDesc", POOL_DTYPE), ("CopyDesc", COPY_DTYPE), ("LossDesc", LOSS_DTYPE),
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
+                     ("WgFinDesc", WGFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
                      ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE), ("AdamCtx", ADAM_CTX_DTYPE)]:
         if sizes[name] != dt.itemsize:
@@ -563,13 +609,32 @@ def conv_wgrad_config(geo: dict, F: int):
         best = max(range(len(CONV_PATCH_TIERS)), key=lambda t_: (min(conv_wgrad_ipc(geo, t_), want), -t_))
         if conv_wgrad_ipc(geo, best) >= 2:
             tier = best
-    kp = KH * KW * cp
-    bmf = 16 if F <= 16 else (32 if F <= 32 else 64)
-    if bmf == 64:
-        bnk = 256 if kp > 128 else 128
-    else:
-        bnk = 512 if kp >= 384 else (256 if kp > 128 else 128)
-    return bmf, min(bnk, CONV_WGRAD_BNK_MAX), tier
+    # (the 64 KB patch tier is built for 16-filter blocks only: two LDS-DMA stages of it fill the CU's LDS)
+    bmf = 16 if F <= 16 or tier == 2 else (32 if F <= 32 else 64)
+    return bmf, conv_wgrad_bnk(KH * KW * cp, bmf), tier
+
+
+def conv_wgrad_bnk(kp: int, bmf: int) -> int:
+    """Columns of the padded (tap, Cp) reduction space one conv WGRAD block covers (gemm3.hip: 4 waves x
+    NTW = BNK / 64 column tiles of 16, every wave all BMF filters): the whole width when the accumulators
+    allow it (TF x NTW <= 32 tiles of 4 registers per lane), so the staged patch of a chunk -- the kernel's
+    dominant traffic -- is read once for every tap; at least 2 tiles per wave."""
+    ntw_max = max(2, min(CONV_WGRAD_BNK_MAX // 64, 32 // (bmf // 16)))
+    ntw = 2
+    while ntw < ntw_max and 64 * ntw < kp:
+        ntw *= 2
+    return 64 * ntw
+
+
+def conv_wgrad_splits(nchunks: int, wave_mfmas_per_chunk: int) -> int:
+    """Chunk-range splits of one conv WGRAD problem (gemm3.hip g3_conv_wgrad_kernel): enough that no block
+    runs more than CONV_WGRAD_WAVE_MFMAS MFMAs per wave or CONV_WGRAD_MAX_CHUNKS chunks (a chunk's patch
+    staging is latency-bound, so narrow problems are bounded by chunks, wide ones by MFMAs), and at least
+    CONV_WGRAD_MIN_CHUNKS chunks per block.  The splits meet in per-split fp32 slabs summed in order by the
+    wgrad_finalize launch, so their cost is slab bytes (plain stores), not fixed-point atomics.  A function of
+    the problem alone (deterministic: the split boundaries decide the partial sums)."""
+    want = max(-(-nchunks * wave_mfmas_per_chunk // CONV_WGRAD_WAVE_MFMAS), -(-nchunks // CONV_WGRAD_MAX_CHUNKS))
+    return max(1, min(want, nchunks // CONV_WGRAD_MIN_CHUNKS))
 
 
 NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
@@ -675,7 +740,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
         if mode == MODE_WGRAD and v is None:
             cfg = conv_wgrad_config(r, M)
             if cfg is not None:
-                v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1]
+                v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1] // 64   # (BNK / 64: column tiles per wave)
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
             if mode == MODE_WGRAD and WGRAD_WIDE and 64 < M <= 192 and N > 16 and v < 1000000 \
@@ -713,7 +778,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tl.append(np.stack([np.full(bb.size, p), bb.ravel(), jj.ravel() * tm, nn.ravel()], 1))
             tiles = np.concatenate(tl).astype(np.int32)
         elif v >= 3000000 and mode == MODE_WGRAD:
-            bmf, bnk = (v % 100000) // 1000, v % 1000
+            bmf, bnk = (v % 100000) // 1000, 64 * (v % 1000)
             tl = []
             tier = (v // 100000) % 10
             geo = []
@@ -722,9 +787,22 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 ipc = conv_wgrad_ipc(r, tier)
                 nchunks = -(-(K // ohw) // ipc) if ipc >= 2 else (K // ohw) * (-(-ohw // 128))
                 cp = -(-int(r["C"]) // 8) * 8
-                nkt = -(-(int(r["KH"]) * int(r["KW"]) * cp) // bnk)
+                ldp = int(r["KH"]) * int(r["KW"]) * cp
+                nkt = -(-ldp // bnk)
                 nft = -(-M // bmf)
-                geo.append((nchunks, nkt, nft, min(CONV_WGRAD_MAXPER, max(8, -(-nchunks // CONV_WGRAD_SPLITS)))))
+                # MFMAs per wave and chunk of the widest block: 4 k steps x f tiles x its column tiles, taken
+                # in groups of 4 per wave
+                ntw = bnk // 64
+                nvj = -(-min(4 * ntw, -(-ldp // 16)) // 4)
+                per = -(-nchunks // conv_wgrad_splits(nchunks, 4 * (bmf // 16) * 4 * -(-nvj // 4)))
+                ns = -(-nchunks // per)
+                r["kper"] = per
+                if ns > 1:
+                    r["_wgfin"] = ns                # fp32 slabs + wgrad_finalize (the caller allocates ext)
+                    r["_ldp"] = ldp
+                else:
+                    r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
+                geo.append((nchunks, nkt, nft, per))
             # (chunks per block 8..64: unlike the GEMM WGRAD, more and shorter blocks measured slower --
             # every block restages its patches and the cross-chunk prefetch needs a long chunk range)
             for p, (r, (M, N, K)) in enumerate(items):
@@ -737,7 +815,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 t_[..., 1] = fk[None, :]
                 t_[..., 2] = c0[:, None]
                 t_[..., 3] = np.minimum(nchunks, c0 + per)[:, None]
-                tl.append(t_.reshape(-1, 4))
+                # the f x k' tiles of one chunk range stage the same input patches: one XCD (its L2) for them
+                tl.append(xcd_swizzle(t_.reshape(-1, 4), len(fk)))
             tiles = np.concatenate(tl).astype(np.int32)
         else:
             bm, bn = gemm3_block(mode, v)
@@ -780,6 +859,19 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000)
         out.append((v, [r for r, _ in items], tiles))
     return out
+
+
+def wgrad_finalize_row(r: dict, ws_ptr: int, adam: int = 0) -> dict:
+    """WgFinDesc of a split conv WGRAD row (``_wgfin`` set by gemm3_plan) whose slabs live at ``ws_ptr``
+    (``wgrad_slab_elems(r)`` fp32); sets the row's ``ext``."""
+    r["ext"] = ws_ptr
+    C = int(r["C"])
+    return dict(ws=ws_ptr, out=int(r["out"]), adam=adam, M=int(r["M"]), N=int(r["N"]), C=C, Cp=-(-C // 8) * 8,
+                S=int(r["_wgfin"]), flags=0)
+
+
+def wgrad_slab_elems(r: dict) -> int:
+    return int(r["_wgfin"]) * int(r["M"]) * int(r["_ldp"])
 
 
 def dgrad_reads_natural(KH: int, KW: int, SH: int, SW: int, F: int) -> bool:
@@ -848,11 +940,12 @@ WGRAD_WIDE_MAXK = int(_os.environ.get("SERANN_WGRAD_WIDE_MAXK", "64"))
 # m-split WGRAD problems run two row groups of 4 waves per block (gemm3.hip, variant + 500): a block walks
 # 2 x 128 k-steps, so an m-split costs one fixed-point flush per 256 k-steps at the same parallelism
 WGRAD_ROW_GROUPS = int(_os.environ.get("SERANN_WGRAD_ROW_GROUPS", "2"))
-# conv-halo WGRAD: chunk-range splits per problem (8..CONV_WGRAD_MAXPER 128-row chunks per block)
-CONV_WGRAD_SPLITS = int(_os.environ.get("SERANN_CONV_WGRAD_SPLITS", "64"))
-CONV_WGRAD_MAXPER = int(_os.environ.get("SERANN_CONV_WGRAD_MAXPER", "64"))
-# k' tile width cap: 256 measured 14.56 vs 14.61 ms (4 streams), 18.3 vs 18.6 (1 stream), 12 fewer launches
-CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "256"))
+# conv-halo WGRAD chunk-range splits (conv_wgrad_splits): per-block bounds on MFMAs per wave and on chunks
+CONV_WGRAD_WAVE_MFMAS = int(_os.environ.get("SERANN_CONV_WGRAD_WAVE_MFMAS", "4096"))
+CONV_WGRAD_MAX_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MAX_CHUNKS", "8"))
+CONV_WGRAD_MIN_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MIN_CHUNKS", "4"))
+# column width cap of a conv WGRAD block (round 5: 1024, i.e. 16 column tiles per wave for 16-filter problems)
+CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "2048"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 

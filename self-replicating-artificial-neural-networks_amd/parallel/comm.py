@@ -53,6 +53,16 @@ class Comm:
     def allreduce_max(self, value: float) -> float:
         return value
 
+    def device_index(self) -> int:
+        """Index of the GPU this rank computes on, or -1 (CPU)."""
+        try:
+            import torch
+            if torch.cuda.is_available():
+                return int(torch.cuda.current_device())
+        except ImportError:
+            pass
+        return -1
+
     def shutdown(self):
         pass
 
@@ -147,6 +157,9 @@ class TorchDistComm(Comm):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def device_index(self) -> int:
+        return int(self.device.index) if self.device.type == "cuda" else -1
+
     def shutdown(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group()
@@ -188,13 +201,17 @@ def _host_bytes(body) -> bytes:
     return np.ascontiguousarray(body, np.uint8).tobytes()
 
 
+_HEAD_INTS, _HEAD_TIMES = 4, 3       # (n, pool, L, device index), (learning, replication, shard wall) seconds
+
+
 def pack_header(indices: np.ndarray, metrics: np.ndarray, pool: int, L: int,
-                learning_time: float, replication_time: float) -> bytes:
-    """The host part of a result record: (n, pool, L), the two timings, the organism indices and the
-    (n, 4) float64 metrics.  The packed offspring bits [n][pool][ceil(L / 8)] follow it."""
+                learning_time: float, replication_time: float, device: int = -1, shard_s: float = 0.0) -> bytes:
+    """The host part of a result record: (n, pool, L, the rank's GPU index), three timings (learning,
+    replication, the whole shard's wall time), the organism indices and the (n, 4) float64 metrics.  The
+    packed offspring bits [n][pool][ceil(L / 8)] follow it."""
     n = len(indices)
-    header = np.array([n, pool if n else 0, L if n else 0], dtype=np.int64).tobytes()
-    times = np.array([learning_time, replication_time], dtype=np.float64).tobytes()
+    header = np.array([n, pool if n else 0, L if n else 0, device], dtype=np.int64).tobytes()
+    times = np.array([learning_time, replication_time, shard_s], dtype=np.float64).tobytes()
     return header + times + np.asarray(indices, np.int32).tobytes() + np.asarray(metrics, np.float64).tobytes()
 
 
@@ -209,10 +226,17 @@ def pack_results(indices: np.ndarray, metrics: np.ndarray, offspring: np.ndarray
     return head + bits
 
 
+def unpack_header(payload: bytes) -> dict:
+    """The rank-level fields of a result record: organisms, GPU index and timings."""
+    n, pool, L, dev = np.frombuffer(payload[:8 * _HEAD_INTS], dtype=np.int64)
+    lt, rt, sh = np.frombuffer(payload[8 * _HEAD_INTS:8 * (_HEAD_INTS + _HEAD_TIMES)], dtype=np.float64)
+    return dict(organisms=int(n), device=int(dev), learning_s=float(lt), replication_s=float(rt), shard_s=float(sh))
+
+
 def unpack_results(payload: bytes):
-    n, pool, L = np.frombuffer(payload[:24], dtype=np.int64)
-    lt, rt = np.frombuffer(payload[24:40], dtype=np.float64)
-    off = 40
+    n, pool, L, _dev = np.frombuffer(payload[:8 * _HEAD_INTS], dtype=np.int64)
+    lt, rt, _sh = np.frombuffer(payload[8 * _HEAD_INTS:8 * (_HEAD_INTS + _HEAD_TIMES)], dtype=np.float64)
+    off = 8 * (_HEAD_INTS + _HEAD_TIMES)
     idx = np.frombuffer(payload[off:off + 4 * n], dtype=np.int32)
     off += 4 * n
     metrics = np.frombuffer(payload[off:off + 8 * n * 4], dtype=np.float64).reshape(n, 4)

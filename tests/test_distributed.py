@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, db_path):
+def _worker(rank, world, port, db_path, perf_log=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch
@@ -40,7 +40,8 @@ def _worker(rank, world, port, db_path):
     codec = TableCodec.from_generator(128, seed=1, ancestor=p["ancestor_genotype"])
     w = ShardWorker(p, data, "torch", "cpu", TrainConfig(epochs=1, batch_size=250))
     db = ExperimentDB(db_path) if comm.is_root else None
-    Experiment("dist", enc, w, db, p, codec, comm=comm, random_seed=3, verbose=False).execute()
+    Experiment("dist", enc, w, db, p, codec, comm=comm, random_seed=3, verbose=False,
+               perf_log=perf_log if comm.is_root else None).execute()
     comm.shutdown()
 
 
@@ -56,9 +57,10 @@ def test_gloo_world_matches_world1(tmp_path, world):
     p1 = str(tmp_path / "w1.sqlite")
     _worker(0, 1, _free_port(), p1)
     p2 = str(tmp_path / f"w{world}.sqlite")
+    log = str(tmp_path / f"w{world}.jsonl")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, p2)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, p2, log)) for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -66,6 +68,18 @@ def test_gloo_world_matches_world1(tmp_path, world):
         assert pr.exitcode == 0
     a, b = _read(p1), _read(p2)
     pd.testing.assert_frame_equal(a, b, check_exact=False, rtol=1e-5, atol=1e-6)
+    # the per-generation records explain a multi-GPU run: every rank's device, organisms, predicted and
+    # measured seconds and shard wall time, and the cost of the one collective (bench.py prints these)
+    import json
+    recs = [json.loads(line) for line in open(log)]
+    assert len(recs) == 2
+    for rec in recs:
+        ranks = rec["ranks"]
+        assert [r["rank"] for r in ranks] == list(range(world))
+        assert all(r["device"] == -1 for r in ranks)                     # gloo / CPU ranks
+        assert sum(r["organisms"] for r in ranks) == rec["valid"]
+        assert all(r["shard_s"] >= r["measured_s"] >= 0 and r["predicted_s"] >= 0 for r in ranks)
+        assert rec["allgather_s"] > 0 and rec["allgather_bytes"] > 0
 
 
 def test_rank_speed_model_balances_injected_slowdowns():

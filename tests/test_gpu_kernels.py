@@ -54,10 +54,22 @@ def _run_gemm(mode, rows, dims):
     # reference ops (MIOpen / hipBLASLt) may still be in flight, and the descriptor tables below are
     # uploaded from pageable memory: start every launch from an idle device
     torch.cuda.synchronize()
+    keep = []
     for v, rws, tiles in H.gemm3_plan(mode, [dict(r) for r in rows], dims):
+        fin = []
+        for r in rws:
+            if r.get("_wgfin"):                   # split conv WGRAD: fp32 slabs + the ordered finalize
+                ws = torch.empty(H.wgrad_slab_elems(r) + 64, dtype=torch.float32, device=DEV)
+                keep.append(ws)
+                fin.append(H.wgrad_finalize_row(r, ws.data_ptr()))
         d = _desc([{k: val for k, val in r.items() if not k.startswith("_")} for r in rws], H.GEMM_DTYPE)
         t = torch.as_tensor(tiles, device=DEV)
         H.lib().gemm3(mode, v, d.data_ptr(), t.data_ptr(), len(t), H.stream_handle())
+        if fin:
+            fd = _desc(fin, H.WGFIN_DTYPE)
+            ft = torch.as_tensor(H.chunk_tiles([f["M"] * f["N"] for f in fin], H.WGFIN_ELEMS), device=DEV)
+            H.lib().wgrad_finalize(fd.data_ptr(), ft.data_ptr(), len(ft), H.stream_handle())
+            keep += [fd, ft]
     torch.cuda.synchronize()
 
 
@@ -96,6 +108,12 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     # (5x5 outputs: 3 images per chunk, a ragged last chunk; 8x8 outputs: 2 images per chunk)
     (17, 11, 11, 64, 16, 7, 7, 1, 1, "relu"),
     (9, 12, 12, 32, 24, 5, 5, 1, 1, "linear"),
+    # tap-shifted conv WGRAD (round 5): a whole 2000-column reduction in two 1024-column blocks (16 column
+    # tiles per wave, odd C), 49 taps x 32 channels, 64 filters x 4 column tiles per wave with odd C
+    (6, 28, 28, 74, 16, 5, 5, 1, 1, "relu"),
+    (5, 24, 24, 32, 16, 7, 7, 1, 1, "linear"),
+    (4, 14, 14, 61, 64, 5, 5, 1, 1, "relu"),
+    (3, 24, 24, 16, 16, 5, 5, 2, 2, "sigmoid"),
     # production-batch first layers on a one-channel input (RT = 4 DGRAD into C = 1)
     (750, 28, 28, 1, 32, 7, 7, 1, 1, "linear"),
     (48, 32, 16, 1, 32, 5, 5, 1, 1, "linear"),

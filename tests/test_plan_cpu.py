@@ -213,6 +213,58 @@ def test_adam_skip_mask():
     assert np.array_equal(bits, want)
 
 
+def test_conv_wgrad_splits_per_problem():
+    """Tap-shifted conv WGRAD (round 5): a block covers the whole padded (tap, Cp) width up to 1024 columns;
+    the chunk-range splits are bounded by MFMAs per wave and by chunks per block, are a function of the
+    problem alone, and split problems get fp32 slabs (``_wgfin``: one per split, summed in order by the
+    finalize) while single-split problems store their Q32 gradient (GF_WSTORE)."""
+    def row(B, Hh, Ww, C, F, K):
+        OH, OW = Hh - K + 1, Ww - K + 1
+        return dict(a=0, b=0, out=1, H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=K, KW=K, SH=1, SW=1, M=F,
+                    N=K * K * C, K=B * OH * OW, flags=0), (F, K * K * C, B * OH * OW)
+    big, dbig = row(750, 28, 28, 74, 16, 5)       # 2000 reduction columns: two 1024-column blocks
+    small, dsmall = row(8, 12, 12, 16, 16, 3)
+    assert H.conv_wgrad_config(big, 16)[1] == 2048 and H.conv_wgrad_config(small, 16)[1] == 256
+    alone = {}
+    for rows, dims in (([big], [dbig]), ([small], [dsmall])):
+        for v, rws, tiles in H.gemm3_plan(H.MODE_WGRAD, [dict(r) for r in rows], dims):
+            alone[rws[0]["N"]] = (v, rws[0].get("_wgfin"), rws[0]["kper"], rws[0]["flags"], tiles[:, 1:].tolist())
+    together = {}
+    for v, rws, tiles in H.gemm3_plan(H.MODE_WGRAD, [dict(big), dict(small)], [dbig, dsmall]):
+        for p, r in enumerate(rws):
+            together[r["N"]] = (v, r.get("_wgfin"), r["kper"], r["flags"], tiles[tiles[:, 0] == p][:, 1:].tolist())
+    assert alone == together
+    v, ns, per, flags, tl = alone[25 * 74]
+    nchunks = 750 * 5                                    # 576 pixels per image: 5 chunks of 128
+    assert ns == -(-nchunks // per) > 1 and per <= H.CONV_WGRAD_MAX_CHUNKS and not flags & H.GF_WSTORE
+    assert len(tl) == ns                                 # one 2048-column block (25 x 80 padded) per split
+    v, ns, per, flags, tl = alone[144]
+    assert ns is None and flags & H.GF_WSTORE            # 16 chunks: one block
+
+
+def test_adam_skip_mask_device_matches_host():
+    """The device-built skip mask (difference array over whole groups + edge bits) equals the per-parameter
+    host construction on random disjoint regions: contiguous blocks, strided column slices, ranges inside
+    one 4-parameter group, and ranges that end or start mid-group next to each other."""
+    import torch
+    rng = np.random.default_rng(3)
+    for trial in range(40):
+        n = int(rng.integers(8, 3000))
+        regions, used = [], np.zeros(n, bool)
+        for _ in range(int(rng.integers(1, 12))):
+            rows, cols = int(rng.integers(1, 6)), int(rng.integers(1, 40))
+            ld = cols if rng.random() < 0.5 else cols + int(rng.integers(1, 9))
+            off = int(rng.integers(0, n))
+            idx = off + np.arange(rows)[:, None] * ld + np.arange(cols)[None, :]
+            if idx.max() >= n or used[idx.ravel()].any():
+                continue
+            used[idx.ravel()] = True
+            regions.append((off, rows, cols, ld))
+        want = H.adam_skip_mask(n, regions)
+        got = H.adam_skip_mask_device(n, regions, torch.device("cpu")).numpy()
+        assert np.array_equal(got, want), (trial, regions)
+
+
 def test_wgrad_row_groups_are_per_problem():
     """Dense / 1x1 WGRAD: m-split problems get two row groups per block (variant + 500, twice the k-steps
     per block, half the fixed-point flushes); single-split problems (plain store / fused Adam) keep one.
