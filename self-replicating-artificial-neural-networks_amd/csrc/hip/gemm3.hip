@@ -1098,6 +1098,21 @@ __device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only 
 }
 // LDS-DMA stages of the conv WGRAD ring: 3 when two blocks of them fit a CU's 160 KB (latency hidden by two blocks
 // and two chunks in flight each), else as many as one block can hold (at most 4, at least 2)
+// Channel stride of a conv WGRAD patch pixel: Cp rounded up to an odd number of 16-B slots.  The 8 rows a
+// ds_read_b64_tr_b16 lane group reads are 8 consecutive output pixels (conv_wgrad_row_pixel); at a stride of an
+// odd number of 16-B slots their 32-B windows overlap at most once in the 256-B bank row.  (A stride with
+// SW * Cs = 16 (mod 32), which tiles the bank row exactly, measured no faster and grows the patch up to 50 %:
+// profiles/r5/cwg_isolated_*.log.)  hip_ops.conv_wgrad_cs mirrors it.
+__host__ __device__ constexpr int conv_wgrad_cs(int Cp, int SW) {
+    return ((Cp >> 3) & 1) ? Cp : Cp + 8;
+}
+// Pixel (relative to the chunk's first) of logical row r of a conv WGRAD chunk: inside each 32-row k step the rows
+// a transposing read takes together -- {g * 8 + h * 4 + q : g in {0, 1} or {2, 3}, q < 4} for read h -- are 8
+// consecutive pixels.  dY rows and patch row offsets use the same map, so the MFMA sums the same pairs.
+__device__ __forceinline__ int conv_wgrad_row_pixel(int r) {
+    const int g = (r >> 3) & 3, h = (r >> 2) & 1;
+    return (r & ~31) | ((g >> 1) << 4) | (h << 3) | ((g & 1) << 2) | (r & 3);
+}
 constexpr int conv_wgrad_stages(int stage_bytes) {
     return 3 * stage_bytes <= 80 * 1024 ? 3
            : (4 * stage_bytes <= 160 * 1024 ? 4 : (3 * stage_bytes <= 160 * 1024 ? 3 : 2));
@@ -1127,7 +1142,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const int ohw = g.OH * g.OW;
     const int tpi = (ohw + TM - 1) / TM;
     const int Cp = (g.C + 7) & ~7, C8 = Cp >> 3;
-    const int Cs = (C8 & 1) ? Cp : Cp + 8, Cs8 = Cs >> 3;
+    const int Cs = conv_wgrad_cs(Cp, g.SW), Cs8 = Cs >> 3;
     // q / Cs8 for slot indices q < 2^12 (PATCH / 8): (q * mCs) >> 17, mCs = ceil(2^17 / Cs8), exact for Cs8 <= 32;
     // wider channels use the generic magic (fdiv)
     const uint32_t mCs = (131072u + Cs8 - 1) / (uint32_t)Cs8;
@@ -1191,7 +1206,9 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     // Issue every load of chunk ch into stage st: exactly PER buffer_load ... lds per thread (pieces past the
     // patch / tile load out of range: zeros), and the stage's row offsets (ds_write, ordered by the barrier
     // that precedes the stage's use).
-    auto issue = [&](int ch, int st) {
+    // part: the loads are issued in 4 parts (part < 0: all at once), one per 32-row k step of the chunk being
+    // computed, so their issue cost (~60 cycles per LDS-DMA) interleaves with MFMAs
+    auto issue = [&](int ch, int st, int part) {
         int b, m0, m_last;
         chunk_geom(ch, b, m0, m_last);
         int npix, gbase, oh_a = 0;
@@ -1205,8 +1222,11 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
         }
         bf16_t* const stage = smem + st * STG;
+        constexpr int PQ = (PD + 3) / 4;
+        const int k0 = part < 0 ? 0 : part * PQ, k1 = part < 0 ? PD : min(PD, (part + 1) * PQ);
 #pragma unroll
         for (int k = 0; k < PD; ++k) {
+            if (k < k0 || k >= k1) continue;
             const int q0 = (k * 4 + wave) * 64;          // wave-uniform first slot of this instruction
             const int qq = q0 + lane;
             const int p = small_cs ? (int)(((uint32_t)qq * mCs) >> 17) : fdiv(qq, dCs8);
@@ -1214,13 +1234,14 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             const int off = (p < npix && c8 < C8) ? (gbase + p * g.C + c8 * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_ptr_t)(stage + q0 * 8), 16, off, 0, 0, 0);
         }
+        if (part > 0) return;
         bf16_t* const dyt = stage + PATCH;
 #pragma unroll
         for (int k = 0; k < AD; ++k) {
             const int q0 = (k * 4 + wave) * 64;
             int r, fc;
             tr_swz_piece<NBA>(q0 + lane, r, fc);        // the logical piece the swizzled reads expect here
-            const int m = m0 + r;
+            const int m = m0 + conv_wgrad_row_pixel(r);
             const int off = (m <= m_last && f0 + fc < g.F) ? ((b * ohw + m) * g.F + f0 + fc) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rZ, (lds_ptr_t)(dyt + q0 * 8), 16, off, 0, 0, 0);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rY, (lds_ptr_t)(dyt + DYT + q0 * 8), 16, has_act ? off : OOB,
@@ -1228,7 +1249,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         }
         if (t < TM) {
             // row offsets (rows past the chunk end read a valid pixel: their dZ rows are zero)
-            int m = m0 + t;
+            int m = m0 + conv_wgrad_row_pixel(t);
             if (m > m_last) m = m0;
             const int j = multi ? fdiv(m, g.dOHW) : 0;     // image inside the chunk
             const int pm = m - j * ohw;
@@ -1241,7 +1262,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const int z = td.z, w = td.w;
 #pragma unroll
     for (int s_ = 0; s_ < NST - 1; ++s_)
-        if (z + s_ < w) issue(z + s_, s_);
+        if (z + s_ < w) issue(z + s_, s_, -1);
     int st = 0;
     for (int ch = z; ch < w; ++ch) {
         // retire chunk ch's loads: the chunks issued after it (at most NST - 2) stay in flight
@@ -1251,14 +1272,16 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // row offsets written
         __builtin_amdgcn_s_barrier();
-        // the stage of chunk ch - 1 is free now (every wave is past its reads): refill it
-        if (ch + NST - 1 < w) issue(ch + NST - 1, st == 0 ? NST - 1 : st - 1);
+        // the stage of chunk ch - 1 is free now (every wave is past its reads): refill it, a quarter per k step
+        const bool refill = ch + NST - 1 < w;
+        const int rst = st == 0 ? NST - 1 : st - 1;
         const bf16_t* const patch = smem + st * STG;
         const bf16_t* const dyt = patch + PATCH;
         const bf16_t* const yt = dyt + DYT;
         const int* const rt = reinterpret_cast<const int*>(yt + DYT);
 #pragma unroll
         for (int sub = 0; sub < TM / 32; ++sub) {
+            if (refill) issue(ch + NST - 1, rst, sub);
             const int mr = sub * 32 + grp * 8 + q;
             const bf16_t* p0 = patch + rt[mr];
             const bf16_t* p1 = patch + rt[mr + 4];

@@ -580,12 +580,18 @@ def conv_lds_config(geo: dict, N: int):
     return None
 
 
+def conv_wgrad_cs(C: int, SW: int) -> int:
+    """Channel stride of a conv WGRAD patch pixel in LDS (gemm3.hip conv_wgrad_cs): Cp = ceil8(C) rounded up to
+    an odd number of 16-B slots."""
+    cp = -(-int(C) // 8) * 8
+    return cp if (cp // 8) % 2 == 1 else cp + 8
+
+
 def conv_wgrad_ipc(geo: dict, tier: int) -> int:
     """Whole images per 128-row chunk of the conv WGRAD kernel (gemm3.hip g3_conv_wgrad_kernel):
     min(128 // (OH*OW), patch capacity // (H*W*Cs)) when that is >= 2, else 1 (per-image pixel tiles)."""
     H, W, C, OH, OW = (int(geo[k]) for k in ("H", "W", "C", "OH", "OW"))
-    cp = -(-C // 8) * 8
-    cs = cp if (cp // 8) % 2 == 1 else cp + 8
+    cs = conv_wgrad_cs(C, int(geo.get("SW", 1)))
     ohw = OH * OW
     ipc = min(128 // ohw, CONV_PATCH_TIERS[tier] // (H * W * cs)) if ohw < 128 else 0
     return ipc if ipc >= 2 else 1
@@ -598,15 +604,19 @@ def conv_wgrad_config(geo: dict, F: int):
     if KH * KW <= 1 or "conv_wgrad" in _OFF:
         return None
     cp = -(-C // 8) * 8
-    cs = cp if (cp // 8) % 2 == 1 else cp + 8
-    span = (OW - 1 + 127) // OW
+    cs = conv_wgrad_cs(C, int(geo.get("SW", 1)))
+    # output rows a 128-pixel chunk spans beyond its first (at most the image's), and the input rows they read
+    span = min((OW - 1 + 127) // OW, OH - 1)
     need = (span * SH + KH) * W * cs
     tier = next((i for i, cap in enumerate(CONV_PATCH_TIERS) if need <= cap), None)
     if tier is None:
         return None
+    # the 64 KB tier is built for 16-filter blocks only (two LDS-DMA stages of it fill the LDS): wider layers keep
+    # their whole-F blocks (4 filter tiles per B fragment) on the smaller tiers whenever the patch fits them
+    tiers = range(len(CONV_PATCH_TIERS)) if F <= 16 or tier == 2 else range(2)
     if OH * OW < 128 and "conv_wgrad_multi" not in _OFF:
         want = 128 // (OH * OW)
-        best = max(range(len(CONV_PATCH_TIERS)), key=lambda t_: (min(conv_wgrad_ipc(geo, t_), want), -t_))
+        best = max(tiers, key=lambda t_: (min(conv_wgrad_ipc(geo, t_), want), -t_))
         if conv_wgrad_ipc(geo, best) >= 2:
             tier = best
     # (the 64 KB patch tier is built for 16-filter blocks only: two LDS-DMA stages of it fill the CU's LDS)

@@ -19,7 +19,9 @@ def test_generator_population_matches_fp32_torch_engine():
     from serann.engine.base import TrainConfig
     from serann.engine.hip_engine import HipPopulationEngine
     from serann.engine.torch_engine import TorchPopulationEngine
-    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=15000, n_test=1000, seed=17),
+    # (no class blending / label noise: the converged organisms below must reach 0.95 in one epoch)
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=15000, n_test=1000, seed=17, label_noise=0.0,
+                                                                  mix=0.0),
                            n_train=15000, n_test=1000)
     df = generate(16, seed=2024, validation_genotype_size=100)
     irs = [interpret(code) for code in df["code"]]
