@@ -116,6 +116,13 @@ __device__ __forceinline__ float wsum(const long long* ws, int C, int idx) {
     return fxw_sum<BN_WS_STRIPES>(ws, C, idx);
 }
 
+// BnDesc::pdb targets (serann_hip.h): the producing GEMM's per-channel bias gradient (channel c -> pdb[c]), or
+// with flags 128 / 256 ONE bias element that receives -/+ the sum over every channel: the Dense(units=1)
+// subtracted from / added to the BN input (x = a - Dense(..)): its bias gradient is -sum(dx), taken here in fp32
+// (the bf16 dx the sub's reduction sees left noise ~1000x torch-bf16's on that mathematically-zero sum).
+__device__ __forceinline__ int pdb_index(const BnDesc& d, int c) { return (d.flags & (128 | 256)) ? 0 : c; }
+__device__ __forceinline__ float pdb_sign(const BnDesc& d) { return (d.flags & 128) ? -1.f : 1.f; }
+
 template <int phase>
 __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, float* sB) {
     const int R = (int)d.R, C = (int)d.C;
@@ -338,7 +345,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
             for (int o = C; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
             if (lane < C) {
                 if (phase == 5) {
-                    fx_add(pdb + lane, a);
+                    fx_add(pdb + pdb_index(d, lane), pdb_sign(d) * a);
                 } else {
                     fxw_add(wsw + 2 * lane, a);
                     fxw_add(wsw + 2 * (C + lane), b);
@@ -355,7 +362,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
                     b += r1[g * 8 * C + c + k * C];
                 }
             if (phase == 5) {
-                fx_add(pdb + c, a);
+                fx_add(pdb + pdb_index(d, c), pdb_sign(d) * a);
             } else {
                 fxw_add(wsw + 2 * c, a);
                 fxw_add(wsw + 2 * (C + c), b);
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(256) void bn_kernel(const BnDesc* __restrict__ desc
                 sdz += v;
                 dx[off] = f2bf(v);
             }
-            if (d.pdb) fx_add(reinterpret_cast<long long*>(d.pdb) + c, sdz);   // C > 256: rows of one thread
+            if (d.pdb) fx_add(reinterpret_cast<long long*>(d.pdb) + pdb_index(d, c), pdb_sign(d) * sdz);   // C > 256
         }
     }
     if ((phase == 0 || phase == 4) && C <= 256) {

@@ -452,7 +452,8 @@ struct GcBwdLds {
     static constexpr int LD1 = F1P + 4, LD2 = F2P + 4;          // image row strides (8-B aligned rows)
     static constexpr int DY = 32 * F2P;                          // staged dy rows [32][F2]
     // MODE 2 stages dy only; MODE 3 also the Z1 / dZ1 / dZ2 images
-    static constexpr int PER_WAVE = MODE == 2 ? DY : DY + 2 * 32 * LD1 + 32 * LD2;
+    // (+ the dZ1 low-part image: dW1 takes dZ1 as hi + lo bf16 pairs, below)
+    static constexpr int PER_WAVE = MODE == 2 ? DY : DY + 3 * 32 * LD1 + 32 * LD2;
     // fp32 reduction slots after the loop (alias the per-wave regions)
     static constexpr int RED = MODE == 2 ? 2 * F2P : F2P * F1P + F1P * 16 + F1P + F2P;
     static constexpr int TOTAL = 4 * PER_WAVE > 2 * RED ? 4 * PER_WAVE : 2 * RED;
@@ -515,6 +516,7 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
     gc_lbf16* imgZ1 = sDy + Lds::DY;               // (MODE 3 only)
     gc_lbf16* imgDZ1 = imgZ1 + 32 * LD1;
     gc_lbf16* imgDZ2 = imgDZ1 + 32 * LD1;
+    gc_lbf16* imgDZ1lo = imgDZ2 + 32 * LD2;        // dZ1 - bf16(dZ1), bf16 (MODE 3)
 
     // super-tiles of this wave: st = wave, wave + 4, ...; the first one's dy is requested first
     const int nst = (R1 - R0 + 31) >> 5;
@@ -640,11 +642,19 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
                 dz2[mt] = v;
                 s1[mt] += v;
             }
-            GcFrag dzb[F2K];
+            // dZ2 as a pair of bf16 operands, hi + lo (lo = dZ2 - hi): dZ1 = W2^T dZ2 then carries ~16 bits of
+            // dZ2 instead of 8.  dW1 = sum over rows of dZ1 x genotype is a heavily cancelling sum (BN makes
+            // sum_rows dZ2 = 0): with one bf16 rounding of dZ2 and one of dZ1 it was 3x torch-bf16's error on
+            // the first Conv1D kernel at B = 96 (profiles/r4/diag_bf16_margin.txt).  Two extra MFMAs per 16 rows.
+            GcFrag dzb[F2K], dzl[F2K];
 #pragma unroll
             for (int s = 0; s < F2K; ++s)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) dzb[s].h[j] = gc_bf(dz2[2 * s + (j >> 2)][j & 3]);
+                for (int j = 0; j < 8; ++j) {
+                    const float e = dz2[2 * s + (j >> 2)][j & 3];
+                    dzb[s].h[j] = gc_bf(e);
+                    dzl[s].h[j] = gc_bf(e - bf2f(dzb[s].h[j]));
+                }
             // images: rows lr, channels 16 mt + 4 q .. + 3 (8-B stores)
 #pragma unroll
             for (int mt = 0; mt < T2; ++mt) {
@@ -665,16 +675,27 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
             for (int mt = 0; mt < T1; ++mt) {
                 gc_f32x4_t v = gc_f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
+                for (int s = 0; s < F2K; ++s) v = gc_mma(w2t[mt][s], dzl[s], v);
+#pragma unroll
                 for (int s = 0; s < F2K; ++s) v = gc_mma(w2t[mt][s], dzb[s], v);
                 if constexpr (A1 != ACT_LINEAR) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] *= gc_dact<A1>(z1[mt][r], act1);
                 }
                 db1p[mt] += v;
+                bf16_t hb[4], lb[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    hb[r] = gc_bf(v[r]);
+                    lb[r] = gc_bf(v[r] - bf2f(hb[r]));
+                }
                 gc_u32x2 u;
-                u.x = (uint32_t)gc_bf(v[0]) | ((uint32_t)gc_bf(v[1]) << 16);
-                u.y = (uint32_t)gc_bf(v[2]) | ((uint32_t)gc_bf(v[3]) << 16);
+                u.x = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16);
+                u.y = (uint32_t)hb[2] | ((uint32_t)hb[3] << 16);
                 *(gc_lu32x2*)(&imgDZ1[lr * LD1 + 16 * mt + 4 * q]) = u;
+                u.x = (uint32_t)lb[0] | ((uint32_t)lb[1] << 16);
+                u.y = (uint32_t)lb[2] | ((uint32_t)lb[3] << 16);
+                *(gc_lu32x2*)(&imgDZ1lo[lr * LD1 + 16 * mt + 4 * q]) = u;
             }
         }
         if (MODE == 2) continue;
@@ -705,8 +726,10 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
         }
 #pragma unroll
         for (int m1 = 0; m1 < T1; ++m1) {
-            GcFrag a1;
+            GcFrag a1, a1l;
             gc_tr_read(a1, imgDZ1, LD1, 16 * m1, lane);
+            gc_tr_read(a1l, imgDZ1lo, LD1, 16 * m1, lane);
+            dw1[m1] = gc_mma(a1l, pp, dw1[m1]);
             dw1[m1] = gc_mma(a1, pp, dw1[m1]);
         }
     }

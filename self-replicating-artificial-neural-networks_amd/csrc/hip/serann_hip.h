@@ -105,7 +105,9 @@ struct BnDesc {
                               // GEMM's dZ = dx * act'(x) (x is its output), so its backward reads no Y.
                               // pdb: that GEMM's bias gradient sum(dZ) is taken here, in fp32: when the act
                               // is linear it is mathematically zero (BN removes the mean), and summing the
-                              // bf16-rounded dZ over ~600k rows instead leaves O(sqrt(R) * 2^-9) noise
+                              // bf16-rounded dZ over ~600k rows instead leaves O(sqrt(R) * 2^-9) noise.
+                              // flags 128 / 256: pdb is ONE bias element that receives -/+ sum(dx) over all
+                              // channels (a Dense(units=1) subtracted from / added to the BN input)
     double eps, momentum;
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum

@@ -1289,6 +1289,40 @@ class HipPopulationEngine(PopulationEngine):
                             and uses.get(src.id, 0) == 1 and rec["req"].get(src.id, False)):
                         dz_folded[o][src.id] = H.ACT_CODES[src.attrs["act"]]
 
+        # A Dense(units=1) combined into a BatchNormalization's input by a subtraction (x = a - Dense(..): a mutant
+        # form): its bias gradient is -sum(dx) of the BN, mathematically ~0 for a centred BN.  The BN
+        # backward takes that sum in fp32 (BnDesc flags 128 / 256) and the Dense's WGRAD skips its bias: summed
+        # from the bf16 dx the sub's broadcast reduction sees, it carried ~1000x torch-bf16's error
+        sub_pdb = [dict() for _ in range(P)]            # bn id -> (gemm id, BnDesc flag)
+        pdb_gemms = [set() for _ in range(P)]
+        for o, lay in org_iter():
+            ir = lay.ir
+            rec = mem["orgs"][o]
+            owner = rec["owner"]
+            uses: Dict[int, int] = {}
+            for n in ir.nodes:
+                if n.op == "reshape":
+                    continue
+                for i in n.inputs:
+                    uses[owner.get(i, i)] = uses.get(owner.get(i, i), 0) + 1
+            for n in ir.nodes:
+                if n.op != "bn":
+                    continue
+                sn = ir.node(owner[n.inputs[0]])
+                if sn.op != "sub" or sn.attrs["mode"] != "tt" or uses.get(sn.id, 0) != 1:
+                    continue
+                srcs = [owner.get(i, i) for i in sn.inputs]
+                if srcs[0] == srcs[1]:
+                    continue
+                for pos, gid in enumerate(srcs):
+                    gn = ir.node(gid)
+                    if (gn.op == "gemm" and gn.attrs["kind"] == "dense" and gid in lay.b
+                            and gn.attrs["act"] == "linear" and gn.shape[-1] == 1 and uses.get(gid, 0) == 1
+                            and gid not in rec["fused_convs"] and gid not in rec["gc_nodes"] and rec["req"].get(gid)):
+                        sub_pdb[o][n.id] = (gid, 128 if pos == 1 else 256)
+                        pdb_gemms[o].add(gid)
+                        break
+
         STAGES = ("dgrad", "pool", "bn", "copy", "ew")
         for d in range(maxd, 0, -1):
             wg_rows, wg_dims = [], []
@@ -1340,8 +1374,10 @@ class HipPopulationEngine(PopulationEngine):
                             act = 0 if n.id in dz_folded[o] else H.ACT_CODES[a["act"]]
                         M = B * OH * OW
                         K = KH * KW * C
-                        # a producer folded into its BN's backward gets its bias gradient from there
-                        dbias = gptr(lay.b[n.id]) if n.id in lay.b and n.id not in dz_folded[o] else 0
+                        # a producer folded into its BN's backward gets its bias gradient from there (as does a
+                        # Dense(units=1) subtracted from a BN input: sub_pdb)
+                        dbias = gptr(lay.b[n.id]) if (n.id in lay.b and n.id not in dz_folded[o]
+                                                      and n.id not in pdb_gemms[o]) else 0
                         xin = self._act_ptr(mem, o, n.inputs[0], inputs)
                         vec = (H.GF_VEC_A if F % 8 == 0 else 0) | (H.GF_VEC_B if C % 8 == 0 else 0)
                         ic = raw_conv_imcol(o, n) if not head else None
@@ -1424,6 +1460,10 @@ class HipPopulationEngine(PopulationEngine):
                             pflags |= dz_folded[o][own] << 4
                             if own in lay.b:
                                 base = dict(base, pdb=gptr(lay.b[own]))
+                        elif n.id in sub_pdb[o]:
+                            gid, pf = sub_pdb[o][n.id]
+                            pflags |= pf
+                            base = dict(base, pdb=gptr(lay.b[gid]))
                         if own is None:
                             tasks["bn"].append((o, None, lambda acc, r=base, f=pflags: dict(r, flags=f | 8),
                                                 H.bn_chunks(R, c)))
@@ -1470,7 +1510,13 @@ class HipPopulationEngine(PopulationEngine):
                         bn_red.append(dict(base, flags=pflags))
                         bn_red_cnt.append(H.bn_chunks(R, c, stats=True))
                         # dxt is private to this BN: overwritten (no accumulate); no dx at all without a target
-                        tasks["bn"].append((o, None, lambda acc, r=base, f=pflags, t=own: dict(r, flags=f | (8 if t is None else 0)),
+                        if n.id in sub_pdb[o] and own is not None:
+                            gid, pf = sub_pdb[o][n.id]
+                            base = dict(base, pdb=gptr(lay.b[gid]), flags=pflags | pf)
+                            pf5 = pflags | pf
+                        else:
+                            pf5 = pflags
+                        tasks["bn"].append((o, None, lambda acc, r=base, f=pf5, t=own: dict(r, flags=f | (8 if t is None else 0)),
                                             H.bn_chunks(R, c)))
                         if own is not None:
                             tasks["ew"].append((o, own, lambda acc, r=(mem["grad"].ptr(rec["grad"][own]), dxt, (outer, inner, c)):
