@@ -50,3 +50,37 @@ if os.environ.get("DIAG_BN"):     # moving statistics after the step: engine vs 
             print(f"node {n.id:2d} {k:16s} rel {np.linalg.norm(h - r) / np.linalg.norm(r):.3g}")
             for c in range(min(8, len(r))):
                 print(f"    c{c:2d} ref {r[c]: .6e}  hip {h[c]: .6e}")
+if os.environ.get("DIAG_ACT"):    # gchain_f64_bn_dense: the BN output (node 4) against a numpy fp32 forward
+    mem = eng._debug_mem
+    kind, off = mem["orgs"][0]["act"][4]
+    R = B * 100
+    hy = (mem["act"] if kind == "act" else mem["f32"]).view(off, R * 64).float().cpu().numpy().reshape(R, 64)
+    gg = g.reshape(R, 1).astype(np.float32)
+    z1 = gg * params[2]["kernel"].reshape(1, 64) + params[2]["bias"]
+    xx = np.maximum(z1 @ params[3]["kernel"].reshape(64, 64) + params[3]["bias"], 0)
+    mu, var = xx.mean(0), xx.var(0)
+    ry = (xx - mu) / np.sqrt(var + 1e-3)
+    print("BN out rel", np.linalg.norm(hy - ry) / np.linalg.norm(ry))
+    err = np.abs(hy - ry).max(1)
+    bad = np.argsort(-err)[:10]
+    print("worst rows", [(int(r), float(err[r])) for r in bad])
+    rows_bad = np.where(err > 0.05 * np.abs(ry).max())[0]
+    print("n rows with large error", len(rows_bad), rows_bad[:40])
+    ch = np.argsort(-np.abs(hy - ry).max(0))[:5]
+    print("worst channels", ch, [(float(hy[bad[0], c]), float(ry[bad[0], c])) for c in ch])
+if os.environ.get("DIAG_DUMP"):   # every activation buffer of organism 0 -> npz (compare two runs offline)
+    mem = eng._debug_mem
+    out = {}
+    for nid, ko in mem["orgs"][0]["act"].items():
+        if ko is None:
+            continue
+        kind, off = ko
+        n = int(np.prod(ir.node(nid).shape)) * B
+        out[f"a{nid}"] = (mem["act"] if kind == "act" else mem["f32"]).view(off, n).float().cpu().numpy()
+    for nid, off in mem["orgs"][0]["grad"].items():
+        try:
+            n = int(np.prod(ir.node(nid).shape)) * B
+            out[f"g{nid}"] = mem["grad"].view(off, n).float().cpu().numpy()
+        except Exception as e:  # noqa: BLE001
+            print("grad", nid, e)
+    np.savez(os.environ["DIAG_DUMP"], **out)

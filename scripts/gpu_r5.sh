@@ -44,6 +44,8 @@ stats() {   # keep the kernel statistics of a rocprofv3 run, drop the (large) tr
 STEPS=${STEPS:-tests,bench1}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 has tests && run gputests 1000 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread
+has acc && run acc 500 python -u -m pytest tests/test_gpu_engine.py -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread -k as_accurate
+has kern && run kern 500 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread
 has probe && run probe 60 ./scripts/micro/rsrc_probe
 # testsall: the whole suite without -x (the conftest ends the session at a GPU fault), to see every failure
 has testsall && run gputestsall 1000 python -u -m pytest tests/ -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread

@@ -6,7 +6,7 @@ every launch a lower bound on its time from the problems in its descriptor table
     ideal = max(minimum bytes / HBM_BW, model FLOPs / MFMA_PEAK)
 
 where minimum bytes count every operand read once and every output written once (weights, activations,
-Q32 gradients; the fused-Adam epilogue's p / m / v / bf16 copy), and FLOPs are the GEMM's 2 M N K.  The
+Q40 gradients; the fused-Adam epilogue's p / m / v / bf16 copy), and FLOPs are the GEMM's 2 M N K.  The
 table is sorted by the gap (measured - ideal): where the step's time goes beyond what the work requires.
 
     python scripts/launch_roofline.py gpurun_out/tl/kernel_trace.csv --population-file populations/bench_gen3_pop125.json
@@ -62,7 +62,7 @@ def gemm_cost(mode, r):
     if flags & H.GF_ADAM:
         out = M * N * 26                                      # p, m, v read + written, bf16 copy written
     else:
-        out = M * N * 8                                       # Q32 gradient (one writer or atomics)
+        out = M * N * 8                                       # Q40 gradient (one writer or atomics)
     return dz + y + x + out, fl
 
 

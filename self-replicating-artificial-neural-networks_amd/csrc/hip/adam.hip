@@ -1,5 +1,5 @@
 // Fused multi-tensor Keras-Adam over a flat fp32 parameter arena (K13 / K38).  The gradients arrive in
-// the deterministic Q32 fixed-point arena (common.h fx_*: int64, 2^-32 units) and are converted here.
+// the deterministic Q40 fixed-point arena (common.h fx_*: int64, 2^-40 units) and are converted here.
 //
 // TF ResourceApplyAdam semantics (experiment_worker.py:80): lr_t = lr*sqrt(1-b2^t)/(1-b1^t),
 // m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr_t m / (sqrt(v) + eps).

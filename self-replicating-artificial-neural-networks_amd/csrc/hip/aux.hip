@@ -250,7 +250,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
     }
     if (phase == 5 && tile == 0) {
         for (int c = t; c < C; c += 256) {
-            if (flags & 1) reinterpret_cast<long long*>(d.dgamma)[c] += fx_q(wsum(ws, C, C + c));   // Q32 arena
+            if (flags & 1) reinterpret_cast<long long*>(d.dgamma)[c] += fx_q(wsum(ws, C, C + c));   // Q40 arena
             if (flags & 2) reinterpret_cast<long long*>(d.dbeta)[c] += fx_q(wsum(ws, C, c));
         }
     }
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const LossDesc* __restrict__ 
     __syncthreads();
     if (threadIdx.x < 4) {
         const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        if (v != 0.f) fx_add(reinterpret_cast<long long*>(d.metrics) + threadIdx.x, v);   // Q32 (deterministic)
+        if (v != 0.f) fxm_add(reinterpret_cast<long long*>(d.metrics) + threadIdx.x, v);   // Q32 (deterministic)
     }
 }
 

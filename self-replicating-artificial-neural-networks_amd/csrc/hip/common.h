@@ -55,34 +55,36 @@ __device__ __forceinline__ float act_grad_from_y(float y, int act) {
 // point.  Integer addition is associative and wraps modulo 2^64, so the total is independent of the
 // order in which the atomics land (and of transient overflow): a replayed training step is bitwise
 // reproducible, and so is the population a seeded experiment evolves.
-//  * fx ("Q32", one word): the gradient arena and the loss metrics.  32 fractional bits: resolution
-//    2^-32 = 2.3e-10 absolute (below the bf16 operand noise of any gradient that can move an Adam
-//    update with eps = 1e-4), final sums within +-2^31.  Each contribution is clamped to +-2^30 first
-//    (NaN -> -2^30) so the conversion is always defined.
-//    The RiboAE trainer (riboae/hip_trainer.py) reuses this arena with Keras' eps = 1e-7, where the
-//    argument above is weaker: a gradient element below 2^-33 (1.2e-10) flushes to zero and one near
-//    1e-9 carries ~10 % quantisation error, while Adam scales g / (|g| + 1e-7) to ~1 % of lr there.
-//    Such elements move a parameter by <= 1e-2 lr per step either way (they are the dead tail of the
-//    embedding / Dense gradients); the RiboAE gradient test bounds every parameter's error against fp32.
+//  * fx ("Q40", one word): the gradient arena.  40 fractional bits: resolution 2^-40 = 9.1e-13 absolute, final
+//    sums within +-2^23 (8.4M; a gradient element is O(1e2) at most).  Each contribution is clamped to +-2^22
+//    first (NaN -> -2^22) so the conversion is always defined.  The resolution is what Keras' eps = 1e-7 Adam
+//    needs (the RiboAE trainer shares this arena): a gradient of 1e-10 carries < 1 % quantisation error, where
+//    the former Q32 arena (2.3e-10) flushed it to zero or doubled it.
+//  * fxm ("Q32", one word): the loss metrics (sums over up to an epoch of rows: range +-2^31).
 //  * fxw ("wide", two words hi, lo): BatchNorm statistics (sums of squares over up to 588k rows).  A
 //    contribution q = round(v * 2^32) is split as hi = q >> 32, lo = q & (2^32 - 1) (lo >= 0); the
-//    words are summed separately, total = hi + lo * 2^-32: same resolution, range +-2^63.
+//    words are summed separately, total = hi + lo * 2^-32: resolution 2^-32, range +-2^63.
 typedef unsigned long long u64_t;
-constexpr float FX_SCALE = 4294967296.f;            // 2^32
-constexpr float FX_INV = 2.3283064365386963e-10f;   // 2^-32
+constexpr float FX_SCALE = 1099511627776.f;          // 2^40 (gradient arena)
+constexpr float FX_INV = 9.094947017729282e-13f;     // 2^-40
+constexpr float FX_CLAMP = 4194304.f;                // 2^22
+constexpr float FXW_SCALE = 4294967296.f;            // 2^32 (metrics, wide statistics)
 
 __device__ __forceinline__ long long fx_q(float v) {
-    return llrintf(fminf(fmaxf(v, -1073741824.f), 1073741824.f) * FX_SCALE);
+    return llrintf(fminf(fmaxf(v, -FX_CLAMP), FX_CLAMP) * FX_SCALE);
 }
 __device__ __forceinline__ void fx_add(long long* p, float v) {
     atomicAdd(reinterpret_cast<u64_t*>(p), (u64_t)fx_q(v));
 }
 __device__ __forceinline__ float fx_f(long long q) { return (float)q * FX_INV; }
+__device__ __forceinline__ void fxm_add(long long* p, float v) {
+    atomicAdd(reinterpret_cast<u64_t*>(p), (u64_t)llrintf(fminf(fmaxf(v, -1073741824.f), 1073741824.f) * FXW_SCALE));
+}
 
 __device__ __forceinline__ void fxw_add(long long* p, float v) {
     long long hi, lo = 0;
     if (fabsf(v) < 1.0e9f) {
-        const long long q = llrintf(v * FX_SCALE);
+        const long long q = llrintf(v * FXW_SCALE);
         hi = q >> 32;
         lo = q & 0xffffffffLL;
     } else {                                          // |v| >= 1e9 > 2^24: already an integer (or NaN)

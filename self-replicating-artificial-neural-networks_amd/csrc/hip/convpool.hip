@@ -16,7 +16,7 @@
 // * WGRAD: dW[f][tap] = sum_{b,p} dz[b,p,f] [argmax == w] img[b][pos(p, w) + tap], one MFMA per
 //   (window offset, 32 pooled positions, 16 filters, 16 taps): A = dz masked by the argmax (held in
 //   registers across the window offsets), B = patches from LDS.  The bias gradient is the plain sum
-//   of dz.  The waves' tiles are summed in LDS in wave order and flushed with one Q32 fixed-point
+//   of dz.  The waves' tiles are summed in LDS in wave order and flushed with one Q40 fixed-point
 //   atomic per (block, weight) (deterministic).
 // There is no DGRAD: the input is the raw image.
 //
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
         }
     }
     // D[row = filter][col = tap]: lane holds filters 4*kg + r of tap column col.  The 4 waves' tiles are
-    // summed in LDS in fixed wave order (deterministic), then flushed with one Q32 fixed-point atomic per
+    // summed in LDS in fixed wave order (deterministic), then flushed with one Q40 fixed-point atomic per
     // (block, weight): with one image per wave (4-image blocks) per-wave flushes would cost 4x the atomics.
     constexpr int RW = TT * 16;
     __shared__ float red[NT * 16 * RW];
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void convpool_wgrad_kernel(const ConvPoolDesc*
         }
         __syncthreads();
     }
-    long long* __restrict__ dw = reinterpret_cast<long long*>(d.dw);     // Q32 gradient arena (common.h)
+    long long* __restrict__ dw = reinterpret_cast<long long*>(d.dw);     // Q40 gradient arena (common.h)
     const int tw = tts * 16;
     for (int e = threadIdx.x; e < NT * 16 * tw; e += 256) {
         const int row = e / tw, tap = e - row * tw;

@@ -806,7 +806,7 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
         }
         __syncthreads();
     }
-    long long* gw2 = reinterpret_cast<long long*>(d.dw2);     // Q32 gradient arena (common.h)
+    long long* gw2 = reinterpret_cast<long long*>(d.dw2);     // Q40 gradient arena (common.h)
     long long* gw1 = reinterpret_cast<long long*>(d.dw1);
     long long* gb1 = reinterpret_cast<long long*>(d.db1);
     long long* gb2 = reinterpret_cast<long long*>(d.db2);

@@ -21,7 +21,7 @@
 //   FWD   : Y[m][f]  = act(im2col(X)[m][k] . Wm[f][k] + b[f])
 //   DGRAD : dX[m][c] = sum_{k'=(kh,kw,f)} dZ[b,(ih-kh)/SH,(iw-kw)/SW,f] . Wt[c][k']
 //   WGRAD : dWm[f][k] += sum_m dZ[m][f] . im2col(X)[m][k]      (LDS tiles, transposing LDS reads,
-//           64 rows of m per barrier pair, Q32 fixed-point atomics into the gradient arena for split-m)
+//           64 rows of m per barrier pair, Q40 fixed-point atomics into the gradient arena for split-m)
 // dZ = dY * act'(Y) is formed on the fly from the layer output Y (GemmDesc::aux) in DGRAD / WGRAD.
 #include <type_traits>
 
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
     const int kh = RG > 1 ? ((kt1 - kt0 + 2 * RG - 1) / (2 * RG)) * 2 : kt1 - kt0;
     const int gk0 = min(kt1, kt0 + rg * kh), gk1 = min(kt1, gk0 + kh);
     const int mlim = min(g.K, gk1 * 32);
-    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q40 gradient arena
     const int t = threadIdx.x - rg * NTH, lane = t & 63, wave = t >> 6;
     const int ohw = g.OH * g.OW;
     const int64_t nb = g.K / ohw;                              // batch
@@ -820,11 +820,11 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
         }
     }
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
-    long long* out = reinterpret_cast<long long*>(d.out);     // Q32 gradient arena (common.h fx_*)
+    long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
     if ((g.flags & (GF_WSTORE | GF_ADAM)) == (GF_WSTORE | GF_ADAM)) {
         // sole writer of this tile: apply the optimizer step here (the gradient quantised exactly as the
-        // Q32 arena would hold it) -- the arena-wide Adam pass skips these parameters
+        // Q40 arena would hold it) -- the arena-wide Adam pass skips these parameters
         const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
         const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
         float* __restrict__ P = reinterpret_cast<float*>(ac.p);
@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 // on load latency: ~3.5 us per chunk against ~0.5 us of MFMAs on a 16-filter problem).  Every DMA count is
 // fixed per chunk, so the ring is retired with counted vmcnt waits and raw s_barriers (a __syncthreads would
 // drain every DMA in flight).  Accumulators stay in registers across chunks; the flush writes fp32 split slabs
-// (or the Q32 gradient of a single split); the bias gradient is reduced from the dZ fragments by wave 0 of
+// (or the Q40 gradient of a single split); the bias gradient is reduced from the dZ fragments by wave 0 of
 // the blocks of column range 0.
 // Small outputs (OH*OW < 128, e.g. a 7x7 conv on an 11x11 map: 25 pixels) would leave most of a
 // 128-row chunk empty, so a chunk then covers ipc = min(128 / (OH*OW), PATCH / (H*W*Cs)) whole
@@ -1174,7 +1174,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     const rsrc_t rX = mkrsrc(d.b, (int64_t)nbatch * g.H * g.W * g.C * 2);
     const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
     const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
-    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q40 gradient arena
     const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     const bool has_act = g.act != ACT_LINEAR;
 
@@ -1342,7 +1342,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     // Flush.  Split problems (d.ext = fp32 slab workspace [S][M][taps * Cp], split = td.z / d.kper): plain
     // stores of the block's partial tile in the padded column space; the grouped wgrad_finalize launch adds
     // the splits in order (no fixed-point atomics: at 16 x 1024 columns per block they were ~30x the MFMA
-    // time).  A single split (GF_WSTORE) stores the Q32 gradient dWm[f][tap * C + c] itself.
+    // time).  A single split (GF_WSTORE) stores the Q40 gradient dWm[f][tap * C + c] itself.
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     if (d.ext) {
         const int ldp = taps * Cp;
@@ -1578,7 +1578,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_kernel(const GemmDesc* __
     const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
     const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
-    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
+    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q40 gradient arena
     float acc[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) acc[j] = 0.f;
@@ -1817,7 +1817,7 @@ __global__ __launch_bounds__(256) void g3_narrow_wgrad_sr_kernel(const GemmDesc*
     const bf16_t* __restrict__ dY = reinterpret_cast<const bf16_t*>(d.a);
     const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.b);
     const bf16_t* __restrict__ Yv = reinterpret_cast<const bf16_t*>(d.aux);
-    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q32 gradient arena
+    long long* dbias = reinterpret_cast<long long*>(d.bias);   // Q40 gradient arena
     int ro[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) ro[j] = (8 * i + j) / F;

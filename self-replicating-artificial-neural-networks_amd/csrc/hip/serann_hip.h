@@ -24,7 +24,7 @@ struct GemmDesc {
 // The parameter / gradient / moment arenas of a population engine (same layout, element e of each is the
 // same parameter) and the device Adam scalars, for WGRAD epilogues that apply the optimizer step (GF_ADAM).
 struct AdamCtx {
-    int64_t p, m, v, pbf, g, lr_t;   // fp32, fp32, fp32, bf16, Q32 int64 arenas; device lr_t (float)
+    int64_t p, m, v, pbf, g, lr_t;   // fp32, fp32, fp32, bf16, Q40 int64 arenas; device lr_t (float)
     float b1, b2, eps, pad;
 };
 enum GemmFlags : int64_t {
@@ -32,7 +32,7 @@ enum GemmFlags : int64_t {
     GF_VEC_B = 2,         // B operand chunks are contiguous 8-element vectors
     GF_ACCUM = 4,         // out += result (bf16 read-modify-write)
     GF_OUT_F32 = 8,       // FWD: write fp32 output (heads)
-    GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores of the Q32 gradient instead of atomics
+    GF_WSTORE = 16,       // WGRAD: single m-split -> plain stores of the Q40 gradient instead of atomics
     GF_SPLITWS = 64,      // FWD (LDS-tiled kernel): k range split over blocks; each split stores its raw
                           // fp32 partial tile to the workspace aux[split][M][N]; splitk_finalize sums
                           // the splits in order and applies bias + activation (no atomics, no zeroing)
@@ -80,8 +80,8 @@ void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint
 // Split WGRAD finalize (aux.hip): a WGRAD problem split over S row ranges leaves one fp32 slab per split,
 // ws[S][M][ldp] with ldp = (N / C) * Cp (the kernel's padded (tap, Cp) columns; Cp = C for Dense), written
 // with plain stores; the finalize adds the S slabs IN SPLIT ORDER (bitwise reproducible, no atomics) and
-// stores the Q32 gradient out[M][N] (N = taps * C) -- or, with adam != 0, applies Keras-Adam to those
-// parameters (the gradient quantised as the Q32 arena would hold it; the arena-wide Adam pass skips them).
+// stores the Q40 gradient out[M][N] (N = taps * C) -- or, with adam != 0, applies Keras-Adam to those
+// parameters (the gradient quantised as the Q40 arena would hold it; the arena-wide Adam pass skips them).
 struct WgFinDesc { int64_t ws, out, adam, M, N, C, Cp, S, ldo, flags; };   // ldo: out row stride (0: N)
 constexpr int WGFIN_ELEMS = 64;       // outputs per block
 void launch_wgrad_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
@@ -97,7 +97,7 @@ struct TransDesc { int64_t src, dst, F, P, C; };                             // 
 constexpr int BN_WS_STRIPES = 8;
 struct BnDesc {
     int64_t x, y, dy, dx, gamma, beta, mm, mv, mean, invstd, ws, dgamma, dbeta;
-    int64_t pdb;              // phase 5: Q32 bias gradient of the GEMM producing x (0 = none), reduced from
+    int64_t pdb;              // phase 5: Q40 bias gradient of the GEMM producing x (0 = none), reduced from
                               // the fp32 dZ before it is rounded to bf16 (serann_hip.h note below)
     int64_t R, C, flags;      // flags: 1 has_gamma, 2 has_beta, 4 accumulate dx, 8 no dx, 64 moving variance
                               // with n / (n - 1) (standard BN) instead of BatchNormalizationF16's n / (n - 1 - eps),
@@ -148,7 +148,7 @@ struct RepBitsDesc { int64_t logits, out, rows, NC, L; };
 // Fused raw-input Dense (K <= 4 input channels, 8 <= F <= 256 units) -> BatchNormalization, training
 // (nbn.hip).  x: the raw input rows (bf16, row stride ldx); w: bf16 [F][K]; bias fp32 (0 = none); y: the BN
 // output; dy: its gradient; ws / wsb: forward / backward wide statistics workspaces (BnDesc layout);
-// dw, db, dgamma, dbeta: Q32 gradient arena (0 = none); flags as BnDesc (1 gamma, 2 beta, 64 n/(n-1)).
+// dw, db, dgamma, dbeta: Q40 gradient arena (0 = none); flags as BnDesc (1 gamma, 2 beta, 64 n/(n-1)).
 struct NbnDesc {
     int64_t x, w, bias, y, dy, gamma, beta, mm, mv, mean, invstd, ws, wsb, dw, db, dgamma, dbeta;
     int64_t R, F, K, ldx, act, flags;

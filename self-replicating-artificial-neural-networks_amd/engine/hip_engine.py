@@ -409,7 +409,7 @@ class HipPopulationEngine(PopulationEngine):
             self.wt_off.append(d)
         self.wt = torch.zeros(max(wt_size, ALIGN) + SLACK, dtype=torch.bfloat16, device=dev)
         self.p = self.parena.materialize()
-        # gradients: deterministic Q32 fixed-point accumulator (csrc/hip/common.h fx_*), converted by Adam
+        # gradients: deterministic Q40 fixed-point accumulator (csrc/hip/common.h fx_*), converted by Adam
         self.g = torch.zeros(self.p.numel(), dtype=torch.int64, device=dev)
         self.m = torch.zeros_like(self.p)
         self.v = torch.zeros_like(self.p)
@@ -790,7 +790,7 @@ class HipPopulationEngine(PopulationEngine):
             return self.p.data_ptr() + off * 4
 
         def gptr(off):
-            return self.g.data_ptr() + off * 8          # Q32 int64 gradient arena
+            return self.g.data_ptr() + off * 8          # Q40 int64 gradient arena
 
         def sptr(off):
             return self.stats.data_ptr() + off * 4
@@ -1863,7 +1863,7 @@ class HipPopulationEngine(PopulationEngine):
         bwd = Plan()
         bwd.launches = plan.launches[plan.fwd_count:]
         bwd.run()
-        grads = (self.g.double() / 2.0 ** 32).float()
+        grads = H.from_qg(self.g)
         if apply_adam:
             c = self.cfg
             self.lib.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),

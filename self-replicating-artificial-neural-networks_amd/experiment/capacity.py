@@ -32,7 +32,7 @@ MIN_GPU_MEMORY_MB = 6000                   # reference admission threshold (run_
 def organism_device_bytes(ir, batch: int, replication_batch: int = 0) -> int:
     """Conservative device footprint of one organism in the HIP engine at training batch ``batch``.
 
-    Parameters: fp32 master + Q32 int64 gradient + 2 fp32 Adam moments + bf16 compute copy + bf16
+    Parameters: fp32 master + Q40 int64 gradient + 2 fp32 Adam moments + bf16 compute copy + bf16
     transposed copy = 24 B per weight.  Activations: bf16 output and bf16 gradient of every node at the
     batch (fused producers never materialise theirs, which this estimate ignores), the uint8 pool
     argmax, fp32 head logits, the split-K FWD workspaces of long-K merged Dense layers (<= 16 fp32

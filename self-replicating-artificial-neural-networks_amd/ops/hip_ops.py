@@ -175,17 +175,24 @@ def bn_ws_words(channels: int) -> int:
     return BN_WS_STRIPES * 2 * int(channels) * 2
 
 
-Q32 = float(2 ** 32)   # csrc/hip/common.h fx_*: the gradient arena and loss metrics are int64 in 2^-32 units
+Q32 = float(2 ** 32)   # csrc/hip/common.h fxm_add: the loss metrics are int64 in 2^-32 units
+QG = float(2 ** 40)    # csrc/hip/common.h fx_*: the gradient arena is int64 in 2^-40 units
+QG_CLAMP = 2.0 ** 22   # fx_q clamps every contribution to +-2^22
 
 
-def to_q32(t):
-    """float tensor -> int64 Q32 fixed point (the kernels' fx_q: clamp to +-2^30, round to nearest)."""
+def to_qg(t):
+    """float tensor -> int64 gradient-arena fixed point (the kernels' fx_q: clamp, round to nearest)."""
     import torch
-    return torch.round(t.double().clamp(-2.0 ** 30, 2.0 ** 30) * Q32).to(torch.int64)
+    return torch.round(t.double().clamp(-QG_CLAMP, QG_CLAMP) * QG).to(torch.int64)
+
+
+def from_qg(t):
+    """int64 gradient-arena tensor (device or host) -> float32 torch tensor on the same device."""
+    return (t.double() / QG).float()
 
 
 def from_q32(t) -> np.ndarray:
-    """int64 Q32 tensor -> float64 numpy array."""
+    """int64 Q32 tensor (loss metrics) -> float64 numpy array."""
     return t.detach().cpu().numpy().astype(np.float64) / Q32
 
 

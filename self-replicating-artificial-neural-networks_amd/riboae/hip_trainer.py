@@ -12,7 +12,7 @@ Convolutions and Dense layers are gemm3 FWD / DGRAD / WGRAD launches (NHWC bf16 
 accumulation), BatchNormalization the bn_kernel phases (train statistics in wide fixed point, moving
 statistics with the standard n / (n - 1) factor), the embedding gradient a WGRAD of the one-hot token
 matrix against the embedding-output gradient, and Adam the fused arena kernel (K13/K38) over a flat fp32
-parameter arena with a Q32 fixed-point gradient arena -- so a step is bitwise reproducible.
+parameter arena with a Q40 fixed-point gradient arena -- so a step is bitwise reproducible.
 
 The torch model's parameters and BatchNorm running statistics are re-pointed into the arenas
 (convolution kernels as permuted views of the output-major layout the kernels use), so the model object
@@ -80,7 +80,7 @@ class HipRiboTrainer:
         return self.plans[B]
 
     # ------------------------------------------------------------------------------------------------
-    # parameter arena: fp32 master, Q32 int64 gradients, Adam moments, bf16 compute copy
+    # parameter arena: fp32 master, Q40 int64 gradients, Adam moments, bf16 compute copy
     # ------------------------------------------------------------------------------------------------
     def _build_params(self):
         m, dev = self.model, self.dev
@@ -394,7 +394,7 @@ class HipRiboTrainer:
              prior_temperature: Optional[float] = None, noise: Optional[torch.Tensor] = None,
              seed: Optional[int] = None, update: bool = True) -> Dict[str, torch.Tensor]:
         """One NELBO training step on a [B][L] token batch; returns device scalars (loss, nll, kld).
-        ``update=False`` leaves the Q32 gradient arena filled and skips Adam (numerics tests)."""
+        ``update=False`` leaves the Q40 gradient arena filled and skips Adam (numerics tests)."""
         B = int(tokens.shape[0])
         L, E, G, A, V = self.L, self.E, self.G, self.A, self.V
         if tuple(tokens.shape) != (B, L):
@@ -501,7 +501,7 @@ class HipRiboTrainer:
         array}, plus the step's (loss, nll, kld).  The BatchNorm moving statistics are restored."""
         st0 = self.stats.clone()
         res = self.step(tokens, temperature, kld_weight, 0.0, noise=noise, update=False)
-        g = (self.g.double() / 2.0 ** 32).float()
+        g = H.from_qg(self.g)
         self.g.zero_()
         with torch.no_grad():
             self.stats.copy_(st0)

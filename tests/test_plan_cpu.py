@@ -217,7 +217,7 @@ def test_conv_wgrad_splits_per_problem():
     """Tap-shifted conv WGRAD (round 5): a block covers the whole padded (tap, Cp) width up to 1024 columns;
     the chunk-range splits are bounded by MFMAs per wave and by chunks per block, are a function of the
     problem alone, and split problems get fp32 slabs (``_wgfin``: one per split, summed in order by the
-    finalize) while single-split problems store their Q32 gradient (GF_WSTORE)."""
+    finalize) while single-split problems store their Q40 gradient (GF_WSTORE)."""
     def row(B, Hh, Ww, C, F, K):
         OH, OW = Hh - K + 1, Ww - K + 1
         return dict(a=0, b=0, out=1, H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=K, KW=K, SH=1, SW=1, M=F,
