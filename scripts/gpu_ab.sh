@@ -1,28 +1,26 @@
 #!/bin/bash
-# A/B of the current in-tree kernels against ab/prev (built by scripts/ab_build.sh): interleaved
-# step-time runs, then per-launch timings of both.
-mkdir -p gpurun_out
+# A/B of environment knobs on the step time of the two fixed populations.  AB="name1:ENV=V ENV2=V;name2:..."
+# (each configuration runs both populations at 4 and 1 streams; a failing step ends the script)
 export TMPDIR=/tmp
-if [ -n "$TESTS" ]; then
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/ab_tests.log; exit 1; }
-  tail -1 gpurun_out/ab_tests.log
-fi
-for i in 1 2; do
-  for v in new prev; do
-    if [ $v = prev ]; then export SERANN_NATIVE_DIR=$PWD/ab/prev; else unset SERANN_NATIVE_DIR; fi
-    if [ -n "$BENCH" ]; then
-      timeout -k 10 300 python bench.py --steps 2 --warmup 1 > gpurun_out/ab_$v$i.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ab_$v$i.log; exit 1; }
-      tail -1 gpurun_out/ab_$v$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v$i', round(d['seconds_per_generation'],3), [round(g['learning_time'],3) for g in d['generations']])"
-    else
-      timeout -k 10 200 python scripts/bench_step.py --streams ${STREAMS:-4,1} ${STEPARGS} > gpurun_out/ab_$v$i.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ab_$v$i.log; exit 1; }
-      grep streams= gpurun_out/ab_$v$i.log | sed "s/^/$v$i /"
-    fi
+mkdir -p gpurun_out/ab
+IFS=';' read -ra CFGS <<< "$AB"
+for c in "${CFGS[@]}"; do
+  name=${c%%:*}; envs=${c#*:}
+  for pop in ${POPS:-bench_gen3_pop125 ancestor_pop125}; do
+    echo "=== $name $pop ($envs)" | tee -a gpurun_out/ab/ab.log
+    env $envs timeout -k 10 300 python3 scripts/bench_step.py --population-file populations/$pop.json --streams ${STREAMS:-4,1} --epochs 2 > gpurun_out/ab/${name}_$pop.log 2>&1
+    rc=$?
+    grep "streams=" gpurun_out/ab/${name}_$pop.log | tee -a gpurun_out/ab/ab.log
+    if [ $rc -ne 0 ]; then echo "failed rc=$rc"; tail -5 gpurun_out/ab/${name}_$pop.log; exit $rc; fi
   done
 done
-if [ -n "$KB" ]; then
-  for v in new prev; do
-    if [ $v = prev ]; then export SERANN_NATIVE_DIR=$PWD/ab/prev; else unset SERANN_NATIVE_DIR; fi
-    timeout -k 10 200 python scripts/bench_kernels.py --pop 125 --out gpurun_out/kb_$v.json > gpurun_out/kb_$v.log 2>&1 || { echo "kb $v failed"; exit 1; }
-    sed -n 2p gpurun_out/kb_$v.log
+if [ -n "$TL" ]; then
+  for pop in bench_gen3_pop125 ancestor_pop125; do
+    rm -rf gpurun_out/ab/trace
+    env $TL timeout -k 10 300 rocprofv3 --kernel-trace -d $(pwd)/gpurun_out/ab/trace -o run --output-format csv -- python3 \
+        scripts/bench_step.py --population-file populations/$pop.json --streams 1 --epochs 1 > gpurun_out/ab/tl_$pop.log 2>&1 || exit 1
+    f=$(find gpurun_out/ab/trace -name "*kernel_trace.csv" | head -1); cp "$f" gpurun_out/ab/${pop}_s1.csv
+    rm -rf gpurun_out/ab/trace
   done
 fi
+exit 0

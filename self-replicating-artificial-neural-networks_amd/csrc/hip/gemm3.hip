@@ -545,6 +545,86 @@ void g3_direct_kernel(const GemmDesc* __restrict__ descs,
     }
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only (gfx9 encoding; expcnt / lgkmcnt max)
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// Flush of a Dense / 1x1 WGRAD tile (g3_wgrad_kernel, g3_dwgrad_kernel): a lane holds rows frow0 + i * 16 + 4 * (lane / 16)
+// + r and columns kcol0 + j * 16 + lane % 16 of its TF x TK accumulator tiles.  Fused Adam (sole writer), plain
+// Q40 store (sole writer) or fixed-point atomics (m-split).
+template <int TF, int TK>
+__device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x4_t (&acc)[TF][TK], int frow0,
+                                            int kcol0, int lane) {
+    const int c16 = lane & 15, rq = (lane >> 4) * 4;
+    long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
+    const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
+    if ((g.flags & (GF_WSTORE | GF_ADAM)) == (GF_WSTORE | GF_ADAM)) {
+        // sole writer of this tile: apply the optimizer step here (the gradient quantised exactly as the
+        // Q40 arena would hold it) -- the arena-wide Adam pass skips these parameters
+        const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
+        const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
+        float* __restrict__ P = reinterpret_cast<float*>(ac.p);
+        float* __restrict__ Mo = reinterpret_cast<float*>(ac.m);
+        float* __restrict__ Vo = reinterpret_cast<float*>(ac.v);
+        bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
+        const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+        // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
+        // and stored -- element by element, each load waited behind the previous element's stores (the
+        // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
+        // round trips per lane in the epilogue, now TF (one batch of TK x 4 x 3 loads in flight each)
+#pragma unroll
+        for (int i = 0; i < TF; ++i) {
+            float pv[TK][4], mv[TK][4], vv[TK][4];
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = kcol0 + j * 16 + c16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = frow0 + i * 16 + rq + r;
+                    if (col < g.N && row < g.M) {
+                        const int64_t e = e0 + (int64_t)row * ldo + col;
+                        pv[j][r] = P[e];
+                        mv[j][r] = Mo[e];
+                        vv[j][r] = Vo[e];
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = kcol0 + j * 16 + c16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = frow0 + i * 16 + rq + r;
+                    if (col < g.N && row < g.M) {
+                        const int64_t e = e0 + (int64_t)row * ldo + col;
+                        float p_ = pv[j][r], m_ = mv[j][r], v_ = vv[j][r];
+                        adam_elem(p_, m_, v_, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
+                        P[e] = p_; Mo[e] = m_; Vo[e] = v_; Pb[e] = f2bf(p_);
+                    }
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TF; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j) {
+            const int col = kcol0 + j * 16 + c16;
+            if (col >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = frow0 + i * 16 + rq + r;
+                if (row < g.M) {
+                    // GF_WSTORE: this block is the problem's only m-split -> the sole writer
+                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = fx_q(acc[i][j][r]);
+                    else fx_add(out + (int64_t)row * ldo + col, acc[i][j][r]);
+                }
+            }
+        }
+}
+
 // ==================================================================================================
 // WGRAD: dWm[f][k] += sum_m dZ[m][f] * im2col(X)[m][k].  Tile BMF (f) x BNK (k), 64 rows of m per
 // step (two MFMA k-substeps per barrier pair).  Both operands are m-major in memory and are staged
@@ -819,73 +899,160 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
                 if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
         }
     }
-    const int c16 = lane & 15, rq = (lane >> 4) * 4;
-    long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
-    const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
-    if ((g.flags & (GF_WSTORE | GF_ADAM)) == (GF_WSTORE | GF_ADAM)) {
-        // sole writer of this tile: apply the optimizer step here (the gradient quantised exactly as the
-        // Q40 arena would hold it) -- the arena-wide Adam pass skips these parameters
-        const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
-        const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
-        float* __restrict__ P = reinterpret_cast<float*>(ac.p);
-        float* __restrict__ Mo = reinterpret_cast<float*>(ac.m);
-        float* __restrict__ Vo = reinterpret_cast<float*>(ac.v);
-        bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
-        const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
-        // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
-        // and stored -- element by element, each load waited behind the previous element's stores (the
-        // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
-        // round trips per lane in the epilogue, now TF (one batch of TK x 4 x 3 loads in flight each)
+    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane);
+}
+
+// ==================================================================================================
+// Dense / 1x1 stride-1 WGRAD with an LDS-DMA staging ring (round 5).  Same tiles, splits and flush as
+// g3_wgrad_kernel, but the dY (and Y) and X row panels of a 64-row step go global -> LDS by buffer_load ... lds
+// (no VGPR staging, no ds_write): each lane of a wave instruction fetches the 16-B piece the XOR-swizzled
+// transposing reads expect at its lane-linear LDS slot (tr_swz_piece).  NST - 1 steps of loads stay in flight
+// behind the MFMAs; the ring is retired with counted vmcnt waits and raw s_barriers.  act' is applied to the A
+// fragments in registers (HASY: the Y tile is staged beside dY).  Requires F % 8 == 0 and C % 8 == 0 (16-B
+// pieces never straddle a row; hip_ops.dwgrad_ok).
+__host__ __device__ constexpr int dwgrad_stages(int stage_bytes) {
+    return 3 * stage_bytes <= 80 * 1024 ? 3 : (4 * stage_bytes <= 160 * 1024 ? 4 : (3 * stage_bytes <= 160 * 1024 ? 3 : 2));
+}
+template <int BMF, int BNK, bool HASY>
+__global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restrict__ descs,
+                                                        const int4* __restrict__ tiles) {
+    constexpr int TM = 64, NBA = BMF / 16, NBB = BNK / 16;
+    constexpr int AT = TM * BMF, BT = TM * BNK;                 // bf16 elements of the dY (Y) and X tiles
+    constexpr int STG = AT * (HASY ? 2 : 1) + BT;
+    constexpr int NST = dwgrad_stages(STG * 2);
+    static_assert(NST * STG * 2 <= 160 * 1024, "dense WGRAD stages exceed the LDS");
+    constexpr int APC = AT / 8, BPC = BT / 8;                   // 16-B pieces per tile
+    static_assert(APC % 64 == 0 && BPC % 256 == 0, "whole wave instructions per tile");
+    constexpr int AD = (APC + 255) / 256, BD = BPC / 256;       // DMA instructions per thread and step
+    constexpr int PER = AD * (HASY ? 2 : 1) + BD;               // vector-memory ops per thread and step (fixed)
+    constexpr int WR = (BMF >= 64) ? 2 : 1, WC = 4 / WR;
+    constexpr int TF = BMF / WR / 16, TK = BNK / WC / 16;
+    __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STG];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = C (cols), K = rows of the batch
+    const int f0 = td.y * BMF, k0c = td.z * BNK;
+    const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // in units of 32 rows
+    const int mb = kt0 * 32, me = min(g.K, kt1 * 32);
+    const int nstep = (me - mb + TM - 1) / TM;
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wf = wave / WC, wk = wave % WC;
+    const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
+    const rsrc_t rX = mkrsrc(d.b, (int64_t)g.K * g.C * 2);
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);   // Q40 gradient arena
+    const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+    // per-thread piece geometry (fixed over the steps; a step adds m0 rows): A / Y pieces, then X pieces
+    int aoff[AD], arow[AD], boff[BD], brow[BD];
 #pragma unroll
-        for (int i = 0; i < TF; ++i) {
-            float pv[TK][4], mv[TK][4], vv[TK][4];
-#pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                    if (col < g.N && row < g.M) {
-                        const int64_t e = e0 + (int64_t)row * ldo + col;
-                        pv[j][r] = P[e];
-                        mv[j][r] = Mo[e];
-                        vv[j][r] = Vo[e];
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                    if (col < g.N && row < g.M) {
-                        const int64_t e = e0 + (int64_t)row * ldo + col;
-                        float p_ = pv[j][r], m_ = mv[j][r], v_ = vv[j][r];
-                        adam_elem(p_, m_, v_, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
-                        P[e] = p_; Mo[e] = m_; Vo[e] = v_; Pb[e] = f2bf(p_);
-                    }
-                }
-            }
-        }
-        return;
+    for (int k = 0; k < AD; ++k) {
+        const int q0 = ((k * 4 + wave) * 64) % APC;             // (APC < 256: waves repeat pieces -- same data)
+        int r, fc;
+        tr_swz_piece<NBA>(q0 + lane, r, fc);
+        const bool ok = f0 + fc < g.F;
+        aoff[k] = (r * g.F + f0 + fc) * 2;
+        arow[k] = ok ? r : (1 << 30);
     }
+#pragma unroll
+    for (int k = 0; k < BD; ++k) {
+        int r, kc;
+        tr_swz_piece<NBB>((k * 4 + wave) * 64 + lane, r, kc);
+        const bool ok = k0c + kc < g.N;
+        boff[k] = (r * g.C + k0c + kc) * 2;
+        brow[k] = ok ? r : (1 << 30);
+    }
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    auto issue = [&](int step, int st) {
+        const int m0 = mb + step * TM, lim = me - m0;
+        bf16_t* const stage = smem + st * STG;
+#pragma unroll
+        for (int k = 0; k < AD; ++k) {
+            const int q0 = ((k * 4 + wave) * 64) % APC;
+            const int off = arow[k] < lim ? aoff[k] + m0 * g.F * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rZ, (lds_ptr_t)(stage + q0 * 8), 16, off, 0, 0, 0);
+            if constexpr (HASY)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rY, (lds_ptr_t)(stage + AT + q0 * 8), 16, off, 0, 0, 0);
+        }
+        bf16_t* const xt = stage + AT * (HASY ? 2 : 1);
+#pragma unroll
+        for (int k = 0; k < BD; ++k) {
+            const int q0 = (k * 4 + wave) * 64;
+            const int off = brow[k] < lim ? boff[k] + m0 * g.C * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_ptr_t)(xt + q0 * 8), 16, off, 0, 0, 0);
+        }
+    };
+
+    f32x4_t acc[TF][TK];
 #pragma unroll
     for (int i = 0; i < TF; ++i)
 #pragma unroll
-        for (int j = 0; j < TK; ++j) {
-            const int col = k0c + wk * (BNK / WC) + j * 16 + c16;
-            if (col >= g.N) continue;
+        for (int j = 0; j < TK; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = dbias != nullptr && td.z == 0 && wk == 0;
+    float bsum[TF];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = f0 + wf * (BMF / WR) + i * 16 + rq + r;
-                if (row < g.M) {
-                    // GF_WSTORE: this block is the problem's only m-split -> the sole writer
-                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = fx_q(acc[i][j][r]);
-                    else fx_add(out + (int64_t)row * ldo + col, acc[i][j][r]);
+    for (int i = 0; i < TF; ++i) bsum[i] = 0.f;
+
+#pragma unroll
+    for (int s_ = 0; s_ < NST - 1; ++s_)
+        if (s_ < nstep) issue(s_, s_);
+    int st = 0;
+    for (int step = 0; step < nstep; ++step) {
+        const int ahead = min(NST - 2, nstep - 1 - step);       // steps issued after this one (still in flight)
+        if (NST >= 4 && ahead >= 2) wait_vmcnt<(NST >= 4 ? 2 * PER : 0)>();
+        else if (NST >= 3 && ahead >= 1) wait_vmcnt<(NST >= 3 ? PER : 0)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        // the stage of step - 1 is free (every wave is past its reads): refill it with step + NST - 1
+        if (step + NST - 1 < nstep) issue(step + NST - 1, st == 0 ? NST - 1 : st - 1);
+        const bf16_t* const As = smem + st * STG;
+        const bf16_t* const Ys = As + AT;
+        const bf16_t* const Bs = As + AT * (HASY ? 2 : 1);
+#pragma unroll
+        for (int sub = 0; sub < TM / 32; ++sub) {
+            const int mr = sub * 32 + grp * 8 + q;
+            bf16x8_t fa[TF], fb[TK];
+#pragma unroll
+            for (int i = 0; i < TF; ++i) {
+                const int col = wf * (BMF / WR) + i * 16 + 4 * pp;
+                bf16x8_t v = tr_frag(&As[tr_swz<NBA>(mr, col)], &As[tr_swz<NBA>(mr + 4, col)]);
+                if constexpr (HASY) {
+                    const bf16x8_t y = tr_frag(&Ys[tr_swz<NBA>(mr, col)], &Ys[tr_swz<NBA>(mr + 4, col)]);
+                    v = __builtin_bit_cast(bf16x8_t, mul_act_grad(__builtin_bit_cast(uint4, v),
+                                                                  __builtin_bit_cast(uint4, y), g.act));
+                }
+                fa[i] = v;
+                if (do_bias) {
+                    Frag fv;
+                    fv.v = v;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[i] += bf2f(fv.h[e]);
                 }
             }
+#pragma unroll
+            for (int j = 0; j < TK; ++j) {
+                const int col = wk * (BNK / WC) + j * 16 + 4 * pp;
+                fb[j] = tr_frag(&Bs[tr_swz<NBB>(mr, col)], &Bs[tr_swz<NBB>(mr + 4, col)]);
+            }
+#pragma unroll
+            for (int i = 0; i < TF; ++i)
+#pragma unroll
+                for (int j = 0; j < TK; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
+        st = st + 1 == NST ? 0 : st + 1;
+    }
+    if (do_bias) {
+        // lane l holds the 8-row sums of filter l % 16 of each f tile: add the 4 row groups
+#pragma unroll
+        for (int i = 0; i < TF; ++i) {
+            bsum[i] += __shfl_xor(bsum[i], 16, 64);
+            bsum[i] += __shfl_xor(bsum[i], 32, 64);
+            const int f = f0 + wf * (BMF / WR) + i * 16 + lane;
+            if (lane < 16 && f < g.F) fx_add(dbias + f, bsum[i]);
+        }
+    }
+    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane);
 }
 
 // ==================================================================================================
@@ -1091,11 +1258,6 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
 // 128-row chunk empty, so a chunk then covers ipc = min(128 / (OH*OW), PATCH / (H*W*Cs)) whole
 // consecutive images when ipc >= 2 (their input images are one contiguous NHWC range; hip_ops
 // conv_wgrad_ipc mirrors the rule for the tile table).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only (gfx9 encoding; expcnt / lgkmcnt max)
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 // LDS-DMA stages of the conv WGRAD ring: 3 when two blocks of them fit a CU's 160 KB (latency hidden by two blocks
 // and two chunks in flight each), else as many as one block can hold (at most 4, at least 2)
 // Channel stride of a conv WGRAD patch pixel: Cp rounded up to an odd number of 16-B slots.  The 8 rows a
@@ -2344,6 +2506,18 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
     const int4* tp = as_ptr<const int4>(tiles);
     dim3 grid((unsigned)ntiles), block(256);
+    if (mode == MODE_WGRAD && variant >= 5000000) {
+        // LDS-DMA Dense / 1x1 WGRAD: 5000000 + BMF * 1000 + BNK (+ 500: act' from a staged Y tile)
+        const int v = variant - 5000000;
+#define DW3(BMF_, BNK_)                                                                                  \
+    if (v == BMF_ * 1000 + BNK_) { hipLaunchKernelGGL((g3_dwgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
+                                   SERANN_CHECK(hipGetLastError()); return; }                            \
+    if (v == BMF_ * 1000 + BNK_ + 500) { hipLaunchKernelGGL((g3_dwgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
+                                         SERANN_CHECK(hipGetLastError()); return; }
+        DW3(64, 128) DW3(64, 64) DW3(32, 128) DW3(32, 64) DW3(16, 256) DW3(16, 128) DW3(16, 64)
+#undef DW3
+        throw std::runtime_error("gemm3: unknown dense WGRAD variant " + std::to_string(variant));
+    }
     if (mode == MODE_WGRAD && variant >= 4000000) {
         const int k = (variant - 4000000) % 100;
         const bool st = (variant - 4000000) >= 100, sr = (variant - 4000000) >= 200;

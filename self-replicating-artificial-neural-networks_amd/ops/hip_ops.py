@@ -765,7 +765,10 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 # one f tile over the whole layer: the X panel of a column tile is read once, not once per
                 # 64-row f tile (a function of the problem alone: its single split is kept)
                 v = next(b for b in (96, 128, 160, 192) if M <= b) * 1000 + 64
-            if mode == MODE_WGRAD:
+            if mode == MODE_WGRAD and dwgrad_ok(r, M, N, v):
+                # LDS-DMA ring kernel (+ 500: act' from a staged Y tile)
+                v = 5000000 + v + (500 if int(r.get("act", 0)) else 0)
+            elif mode == MODE_WGRAD:
                 bm_, bn_ = gemm3_block(mode, v)
                 if wgrad_row_groups(M, N, K, bm_, bn_) == 2:
                     v += 500
@@ -774,7 +777,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     out = []
     for v in sorted(groups):
         items = groups[v]
-        if (mode == MODE_FWD and 6000 <= v < 7000) or (mode == MODE_WGRAD and v >= 4000000):
+        if (mode == MODE_FWD and 6000 <= v < 7000) or (mode == MODE_WGRAD and 4000000 <= v < 5000000):
             per = NARROW_ROWS if mode == MODE_FWD else NARROW_WROWS
             tl = []
             for p, (r, (M, N, K)) in enumerate(items):
@@ -794,7 +797,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 bb, jj, nn = np.meshgrid(np.arange(nb), np.arange(tpi), np.arange(ntn), indexing="ij")
                 tl.append(np.stack([np.full(bb.size, p), bb.ravel(), jj.ravel() * tm, nn.ravel()], 1))
             tiles = np.concatenate(tl).astype(np.int32)
-        elif v >= 3000000 and mode == MODE_WGRAD:
+        elif 3000000 <= v < 4000000 and mode == MODE_WGRAD:
             bmf, bnk = (v % 100000) // 1000, 64 * (v % 1000)
             tl = []
             tier = (v // 100000) % 10
@@ -839,7 +842,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             bm, bn = gemm3_block(mode, v)
             dms = [dm for _, dm in items]
             if mode == MODE_WGRAD:
-                rg = 2 if (v % 1000000) % 1000 >= 500 else 1
+                rg = DWGRAD_RG if v >= 5000000 else (2 if (v % 1000000) % 1000 >= 500 else 1)
                 tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
@@ -876,6 +879,16 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000)
         out.append((v, [r for r, _ in items], tiles))
     return out
+
+
+def dwgrad_ok(geo: dict, M: int, N: int, v: int) -> bool:
+    """A Dense / 1x1 stride-1 WGRAD the LDS-DMA ring kernel takes (gemm3.hip g3_dwgrad_kernel): a regular
+    (non-gather) tile of >= 64 columns, and 16-B aligned rows of dY (F % 8 == 0) and X (C % 8 == 0)."""
+    if not DWGRAD or v >= 1000000 or v // 1000 not in (16, 32, 64) or v % 1000 not in (64, 128, 256):
+        return False
+    if int(geo.get("KH", 1)) * int(geo.get("KW", 1)) != 1 or int(geo.get("SH", 1)) * int(geo.get("SW", 1)) != 1:
+        return False
+    return int(M) % 8 == 0 and int(N) % 8 == 0 and int(geo.get("C", N)) == int(N)
 
 
 def wgrad_finalize_row(r: dict, ws_ptr: int, adam: int = 0) -> dict:
@@ -963,6 +976,12 @@ CONV_WGRAD_MAX_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MAX_CHUNKS", "8")
 CONV_WGRAD_MIN_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MIN_CHUNKS", "4"))
 # column width cap of a conv WGRAD block (round 5: 1024, i.e. 16 column tiles per wave for 16-filter problems)
 CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "2048"))
+# LDS-DMA Dense / 1x1 WGRAD kernel (round 5) and its k steps per block as a multiple of the WGRAD target.  Off by
+# default: on the fixed populations it measured slower than the register-staged kernel (an act' m-split problem
+# 271 -> 420 us: one 128 KB block per CU against three 8-wave blocks; the big single-split Dense WGRADs have
+# C % 8 != 0 and cannot take it; profiles/r5/ab_dma_dense_wgrad.txt)
+DWGRAD = _os.environ.get("SERANN_DWGRAD", "0") != "0"
+DWGRAD_RG = int(_os.environ.get("SERANN_DWGRAD_RG", "2"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 

@@ -571,3 +571,39 @@ def test_small_gradients_reach_adam_unquantised():
     q32 = torch.round(ref_g.double() * 2.0 ** 32) / 2.0 ** 32
     q32_err = ((adam_update(q32) - want).abs() / want.abs().clamp_min(1e-30))[big]
     assert float(q32_err.max()) > 0.2          # the test discriminates: the Q32 arena fails it
+
+
+@pytest.mark.parametrize("F,C,rows,act", [(16, 264, 750, "linear"), (24, 96, 750, "relu"), (64, 64, 20000, "sigmoid"),
+                                          (120, 200, 3000, "linear"), (8, 64, 100, "relu"), (40, 128, 75000, "linear"),
+                                          (64, 136, 750, "linear"), (32, 72, 4100, "sigmoid")])
+def test_dma_dense_wgrad(F, C, rows, act, monkeypatch):
+    """The LDS-DMA ring Dense WGRAD (gemm3.hip g3_dwgrad_kernel): every (BMF, BNK) instantiation with and without
+    the staged Y tile (act' on the A fragments), ragged f / column tiles and 64-row steps, single split (plain
+    store) and m-splits (fixed-point atomics); gradient and bias gradient against fp32, bitwise repeatable."""
+    monkeypatch.setattr(H, "DWGRAD", True)                  # (off by default: hip_ops.DWGRAD)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = H.padded(torch.randn(rows, C, device=DEV, generator=g).bfloat16())
+    dy = H.padded(torch.randn(rows, F, device=DEV, generator=g).bfloat16())
+    ypre = torch.randn(rows, F, device=DEV, generator=g)
+    y = H.padded((torch.relu(ypre) if act == "relu" else torch.sigmoid(ypre)).bfloat16())
+    yf = y.float()
+    dz = dy.float() * {"relu": (yf > 0).float(), "sigmoid": yf * (1 - yf), "linear": torch.ones_like(yf)}[act]
+    dz = dz.bfloat16().float()
+    geo = dict(H=1, W=1, C=C, OH=1, OW=1, F=F, KH=1, KW=1, SH=1, SW=1)
+    row = dict(a=dy.data_ptr(), b=x.data_ptr(), aux=y.data_ptr() if act != "linear" else 0, act=H.ACT_CODES[act],
+               M=F, N=C, K=rows, flags=H.GF_VEC_A | H.GF_VEC_B, **geo)
+    plans = H.gemm3_plan(H.MODE_WGRAD, [dict(row)], [(F, C, rows)])
+    assert len(plans) == 1 and plans[0][0] >= 5000000, plans[0][0]
+    assert (plans[0][0] % 1000 >= 500) == (act != "linear")
+    res = []
+    for _ in range(2):
+        dw = H.operand((F, C), torch.int64, DEV)
+        db = H.operand(F, torch.int64, DEV)
+        dw.zero_()
+        db.zero_()
+        _run_gemm(H.MODE_WGRAD, [dict(row, out=dw.data_ptr(), bias=db.data_ptr())], [(F, C, rows)])
+        res.append((dw.clone(), db.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    ref = dz.double().t() @ x.double()
+    assert _rel(_q(res[0][0]), ref.float()) < 2e-5
+    assert _rel(_q(res[0][1]), dz.double().sum(0).float()) < 1e-5
