@@ -64,6 +64,7 @@ if has prof; then
   stats gpurun_out/ev/prof gpurun_out/ev/kernel_stats.csv
 fi
 has planprof && run planprof 300 python -u scripts/prof_plan.py --population-file populations/bench_gen3_pop125.json
+has ribotest && run ribotest 400 python -u -m pytest tests/test_riboae_hip_train.py -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread
 has riboae && run riboae 400 python scripts/bench_riboae.py --engine hip
 if has riboprof; then
   rm -rf gpurun_out/ev/riboprof

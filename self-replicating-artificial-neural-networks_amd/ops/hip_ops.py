@@ -643,7 +643,7 @@ def conv_wgrad_bnk(kp: int, bmf: int) -> int:
     return 64 * ntw
 
 
-def conv_wgrad_splits(nchunks: int, wave_mfmas_per_chunk: int) -> int:
+def conv_wgrad_splits(nchunks: int, wave_mfmas_per_chunk: int, tiles: int = 1, slab_bytes: int = 0) -> int:
     """Chunk-range splits of one conv WGRAD problem (gemm3.hip g3_conv_wgrad_kernel): enough that no block
     runs more than CONV_WGRAD_WAVE_MFMAS MFMAs per wave or CONV_WGRAD_MAX_CHUNKS chunks (a chunk's patch
     staging is latency-bound, so narrow problems are bounded by chunks, wide ones by MFMAs), and at least
@@ -651,7 +651,14 @@ def conv_wgrad_splits(nchunks: int, wave_mfmas_per_chunk: int) -> int:
     wgrad_finalize launch, so their cost is slab bytes (plain stores), not fixed-point atomics.  A function of
     the problem alone (deterministic: the split boundaries decide the partial sums)."""
     want = max(-(-nchunks * wave_mfmas_per_chunk // CONV_WGRAD_WAVE_MFMAS), -(-nchunks // CONV_WGRAD_MAX_CHUNKS))
-    return max(1, min(want, nchunks // CONV_WGRAD_MIN_CHUNKS))
+    # ... but no more than CONV_WGRAD_MAX_BLOCKS blocks per problem (tiles = its f x column tiles) and
+    # CONV_WGRAD_MAX_SLAB_MB of fp32 slabs (slab_bytes = one split's slab): a problem with thousands of chunks
+    # (the RiboAE's 350 x 50 maps at batch 512: 8000) fills the GPU with long chunk ranges instead of
+    # thousands of splits whose slabs the finalize must read back (205 MB per step there)
+    cap = max(1, CONV_WGRAD_MAX_BLOCKS // max(1, tiles))
+    if slab_bytes > 0:
+        cap = min(cap, max(1, (CONV_WGRAD_MAX_SLAB_MB << 20) // slab_bytes))
+    return max(1, min(want, cap, nchunks // CONV_WGRAD_MIN_CHUNKS))
 
 
 NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
@@ -814,7 +821,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 # in groups of 4 per wave
                 ntw = bnk // 64
                 nvj = -(-min(4 * ntw, -(-ldp // 16)) // 4)
-                per = -(-nchunks // conv_wgrad_splits(nchunks, 4 * (bmf // 16) * 4 * -(-nvj // 4)))
+                per = -(-nchunks // conv_wgrad_splits(nchunks, 4 * (bmf // 16) * 4 * -(-nvj // 4), nft * nkt,
+                                                      4 * M * ldp))
                 ns = -(-nchunks // per)
                 r["kper"] = per
                 if ns > 1:
@@ -974,6 +982,8 @@ WGRAD_ROW_GROUPS = int(_os.environ.get("SERANN_WGRAD_ROW_GROUPS", "2"))
 CONV_WGRAD_WAVE_MFMAS = int(_os.environ.get("SERANN_CONV_WGRAD_WAVE_MFMAS", "4096"))
 CONV_WGRAD_MAX_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MAX_CHUNKS", "8"))
 CONV_WGRAD_MIN_CHUNKS = int(_os.environ.get("SERANN_CONV_WGRAD_MIN_CHUNKS", "4"))
+CONV_WGRAD_MAX_BLOCKS = int(_os.environ.get("SERANN_CONV_WGRAD_MAX_BLOCKS", "2048"))
+CONV_WGRAD_MAX_SLAB_MB = int(_os.environ.get("SERANN_CONV_WGRAD_MAX_SLAB_MB", "64"))
 # column width cap of a conv WGRAD block (round 5: 1024, i.e. 16 column tiles per wave for 16-filter problems)
 CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "2048"))
 # LDS-DMA Dense / 1x1 WGRAD kernel (round 5) and its k steps per block as a multiple of the WGRAD target.  Off by

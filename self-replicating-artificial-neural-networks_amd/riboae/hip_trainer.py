@@ -66,6 +66,7 @@ class HipRiboTrainer:
         self.L, self.E, self.G, self.A, self.V = inf.max_len, inf.emb_dim, inf.genotype_length, inf.alphabet, gen.vocab
         self._build_params()
         self.plans: Dict[int, _Plan] = {}
+        self.keep: List[torch.Tensor] = []          # split-WGRAD slabs referenced by the launch descriptors
 
     def _plan(self, B: int) -> _Plan:
         if B not in self.plans:
@@ -230,9 +231,25 @@ class HipRiboTrainer:
     def _gemm(self, mode, rows, dims, splitk=False):
         out = []
         for v, rws, tiles in H.gemm3_plan(mode, [dict(r) for r in rows], dims, splitk=splitk):
+            # split conv WGRADs: fp32 slabs per split, summed in split order by one wgrad_finalize launch
+            # after the GEMM (without them the splits would meet in fixed-point atomics: 3x slower here)
+            fin = []
+            for r in rws:
+                if r.get("_wgfin"):
+                    ws = _zeros(H.wgrad_slab_elems(r), torch.float32, self.dev)
+                    self.keep.append(ws)
+                    fin.append(H.wgrad_finalize_row(r, ws.data_ptr()))
             clean = [{k: val for k, val in r.items() if not k.startswith("_")} for r in rws]
             d = torch.as_tensor(np.frombuffer(H.gemm_desc_array(clean).tobytes(), dtype=np.uint8).copy(), device=self.dev)
             out.append(("gemm3", (mode, v), d, torch.as_tensor(np.ascontiguousarray(tiles), device=self.dev)))
+            if fin:
+                a = np.zeros(len(fin), dtype=H.WGFIN_DTYPE)
+                for i, f in enumerate(fin):
+                    for k, val in f.items():
+                        a[i][k] = val
+                fd = torch.as_tensor(np.frombuffer(a.tobytes(), dtype=np.uint8).copy(), device=self.dev)
+                ft = torch.as_tensor(H.chunk_tiles([f["M"] * f["N"] for f in fin], H.WGFIN_ELEMS), device=self.dev)
+                out.append(("wgfin", 0, fd, ft))
         return out
 
     def _bn_row(self, bname, x, y, dy, dx, R):
@@ -389,6 +406,8 @@ class HipRiboTrainer:
                 L_.bn(arg, d.data_ptr(), t.data_ptr(), len(t), s)
             elif kind == "splitfin":
                 L_.splitk_finalize(d.data_ptr(), t.data_ptr(), len(t), s)
+            elif kind == "wgfin":
+                L_.wgrad_finalize(d.data_ptr(), t.data_ptr(), len(t), s)
 
     def step(self, tokens: torch.Tensor, temperature: float, kld_weight: float, lr: float,
              prior_temperature: Optional[float] = None, noise: Optional[torch.Tensor] = None,
