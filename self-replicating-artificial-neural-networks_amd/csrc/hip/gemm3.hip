@@ -927,7 +927,11 @@ __global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restri
     constexpr int PER = AD * (HASY ? 2 : 1) + BD;               // vector-memory ops per thread and step (fixed)
     constexpr int WR = (BMF >= 64) ? 2 : 1, WC = 4 / WR;
     constexpr int TF = BMF / WR / 16, TK = BNK / WC / 16;
-    __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STG];
+    // one __shared__ object per stage, compile-time stage selection (see g3_conv_wgrad_kernel)
+    __shared__ __attribute__((aligned(16))) bf16_t sm0[STG];
+    __shared__ __attribute__((aligned(16))) bf16_t sm1[STG];
+    __shared__ __attribute__((aligned(16))) bf16_t sm2[NST > 2 ? STG : 8];
+    __shared__ __attribute__((aligned(16))) bf16_t sm3[NST > 3 ? STG : 8];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = C (cols), K = rows of the batch
@@ -963,9 +967,8 @@ __global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restri
         brow[k] = ok ? r : (1 << 30);
     }
     typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    auto issue = [&](int step, int st) {
+    auto issue = [&](int step, bf16_t* const stage) __attribute__((always_inline)) {
         const int m0 = mb + step * TM, lim = me - m0;
-        bf16_t* const stage = smem + st * STG;
 #pragma unroll
         for (int k = 0; k < AD; ++k) {
             const int q0 = ((k * 4 + wave) * 64) % APC;
@@ -993,19 +996,17 @@ __global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restri
 #pragma unroll
     for (int i = 0; i < TF; ++i) bsum[i] = 0.f;
 
-#pragma unroll
-    for (int s_ = 0; s_ < NST - 1; ++s_)
-        if (s_ < nstep) issue(s_, s_);
-    int st = 0;
-    for (int step = 0; step < nstep; ++step) {
+    if (nstep > 0) issue(0, sm0);
+    if (NST >= 3 && nstep > 1) issue(1, sm1);
+    if (NST >= 4 && nstep > 2) issue(2, sm2);
+    auto run_step = [&](int step, const bf16_t* const As, bf16_t* const rdst) __attribute__((always_inline)) {
         const int ahead = min(NST - 2, nstep - 1 - step);       // steps issued after this one (still in flight)
         if (NST >= 4 && ahead >= 2) wait_vmcnt<(NST >= 4 ? 2 * PER : 0)>();
         else if (NST >= 3 && ahead >= 1) wait_vmcnt<(NST >= 3 ? PER : 0)>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         // the stage of step - 1 is free (every wave is past its reads): refill it with step + NST - 1
-        if (step + NST - 1 < nstep) issue(step + NST - 1, st == 0 ? NST - 1 : st - 1);
-        const bf16_t* const As = smem + st * STG;
+        if (step + NST - 1 < nstep) issue(step + NST - 1, rdst);
         const bf16_t* const Ys = As + AT;
         const bf16_t* const Bs = As + AT * (HASY ? 2 : 1);
 #pragma unroll
@@ -1040,7 +1041,19 @@ __global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restri
                 for (int j = 0; j < TK; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
-        st = st + 1 == NST ? 0 : st + 1;
+    };
+    for (int step = 0; step < nstep; step += NST) {
+        run_step(step, sm0, NST == 2 ? sm1 : (NST == 3 ? sm2 : sm3));
+        if (step + 1 >= nstep) break;
+        run_step(step + 1, sm1, sm0);
+        if (NST >= 3) {
+            if (step + 2 >= nstep) break;
+            run_step(step + 2, sm2, sm1);
+        }
+        if (NST >= 4) {
+            if (step + 3 >= nstep) break;
+            run_step(step + 3, sm3, sm2);
+        }
     }
     if (do_bias) {
         // lane l holds the 8-row sums of filter l % 16 of each f tile: add the 4 row groups
@@ -1286,14 +1299,23 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     constexpr int TF = BMF / 16, NTW = BNK / 64;
     static_assert(BNK % 256 == 0 || BNK == 128, "column tiles: NTW in {2, 4, 8, 16, 32}");
     constexpr int DYT = TM * BMF;                         // bf16 elements of the dY (and of the Y) tile
-    constexpr int STG = PATCH + 2 * DYT + 2 * TM;         // stage: patch, dY, Y, row offsets (TM ints)
-    constexpr int NST = conv_wgrad_stages(STG * 2);
-    static_assert(NST * STG * 2 <= 160 * 1024, "conv WGRAD stages exceed the LDS");
+    constexpr int STG = PATCH + 2 * DYT;                  // stage: patch, dY, Y (+ the row offsets, TM ints, apart)
+    constexpr int NST = conv_wgrad_stages(STG * 2 + TM * 4);
+    static_assert(NST * (STG * 2 + TM * 4) <= 160 * 1024, "conv WGRAD stages exceed the LDS");
     constexpr int PD = PATCH / 2048;                      // patch DMAs per thread and chunk (16-B pieces / 256)
     constexpr int AD = DYT / 2048;                        // dY DMAs per thread and chunk (as many Y DMAs)
     constexpr int PER = PD + 2 * AD;                      // vector-memory ops per thread and chunk (fixed)
-    // ONE shared array (a second __shared__ object beside LDS-DMA targets makes hipcc drain vmcnt before reads)
-    __shared__ __attribute__((aligned(16))) bf16_t smem[NST * STG];
+    // One __shared__ object per ring stage, and the chunk loop unrolled by NST so every stage is a compile-time
+    // object: the compiler's wait-count pass then sees that a chunk's LDS reads cannot alias the LDS-DMA refilling
+    // another stage.  (With one array indexed by a runtime stage it put s_waitcnt vmcnt(0) in front of every k
+    // step's reads -- each refill's loads were waited for as soon as they were issued.)
+    __shared__ __attribute__((aligned(16))) bf16_t sm0[STG];
+    __shared__ __attribute__((aligned(16))) bf16_t sm1[STG];
+    __shared__ __attribute__((aligned(16))) bf16_t sm2[NST > 2 ? STG : 8];
+    __shared__ __attribute__((aligned(16))) bf16_t sm3[NST > 3 ? STG : 8];
+    // the per-stage row offsets are objects of their own too: written with ds_write, they would otherwise share an
+    // object with the stage's LDS-DMA and wait for it
+    __shared__ int rt0[TM], rt1[TM], rt2[NST > 2 ? TM : 1], rt3[NST > 3 ? TM : 1];
     const int4 td = tiles[blockIdx.x];
     const GemmDesc& d = descs[td.x];
     const G3 g = geo3(d);                 // WGRAD dims: M = F (rows), N = KH*KW*C (cols), K = B*OH*OW
@@ -1370,7 +1392,7 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
     // that precedes the stage's use).
     // part: the loads are issued in 4 parts (part < 0: all at once), one per 32-row k step of the chunk being
     // computed, so their issue cost (~60 cycles per LDS-DMA) interleaves with MFMAs
-    auto issue = [&](int ch, int st, int part) {
+    auto issue = [&](int ch, bf16_t* const stage, int* const rtab, int part) __attribute__((always_inline)) {
         int b, m0, m_last;
         chunk_geom(ch, b, m0, m_last);
         int npix, gbase, oh_a = 0;
@@ -1383,7 +1405,6 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             npix = ((oh_b - oh_a) * g.SH + g.KH) * g.W;
             gbase = (b * g.H + oh_a * g.SH) * g.W * g.C;
         }
-        bf16_t* const stage = smem + st * STG;
         constexpr int PQ = (PD + 3) / 4;
         const int k0 = part < 0 ? 0 : part * PQ, k1 = part < 0 ? PD : min(PD, (part + 1) * PQ);
 #pragma unroll
@@ -1417,16 +1438,17 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
             const int pm = m - j * ohw;
             const int oh = fdiv(pm, g.dOW);
             const int ow = pm - oh * g.OW;
-            reinterpret_cast<int*>(stage + PATCH + 2 * DYT)[t] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
+            rtab[t] = j * hwcs + ((oh - oh_a) * g.SH * g.W + ow * g.SW) * Cs;
         }
     };
 
     const int z = td.z, w = td.w;
-#pragma unroll
-    for (int s_ = 0; s_ < NST - 1; ++s_)
-        if (z + s_ < w) issue(z + s_, s_, -1);
-    int st = 0;
-    for (int ch = z; ch < w; ++ch) {
+    if (z < w) issue(z, sm0, rt0, -1);
+    if (NST >= 3 && z + 1 < w) issue(z + 1, sm1, rt1, -1);
+    if (NST >= 4 && z + 2 < w) issue(z + 2, sm2, rt2, -1);
+    // one chunk: its loads retired, then 4 k steps on stage cur while stage rdst (chunk ch - 1's) is refilled
+    auto chunk = [&](int ch, const bf16_t* const patch, const int* const rt, bf16_t* const rdst, int* const rtdst)
+                     __attribute__((always_inline)) {
         // retire chunk ch's loads: the chunks issued after it (at most NST - 2) stay in flight
         const int ahead = min(NST - 2, w - 1 - ch);
         if (NST >= 4 && ahead >= 2) wait_vmcnt<(NST >= 4 ? 2 * PER : 0)>();
@@ -1436,14 +1458,11 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
         __builtin_amdgcn_s_barrier();
         // the stage of chunk ch - 1 is free now (every wave is past its reads): refill it, a quarter per k step
         const bool refill = ch + NST - 1 < w;
-        const int rst = st == 0 ? NST - 1 : st - 1;
-        const bf16_t* const patch = smem + st * STG;
         const bf16_t* const dyt = patch + PATCH;
         const bf16_t* const yt = dyt + DYT;
-        const int* const rt = reinterpret_cast<const int*>(yt + DYT);
 #pragma unroll
         for (int sub = 0; sub < TM / 32; ++sub) {
-            if (refill) issue(ch + NST - 1, rst, sub);
+            if (refill) issue(ch + NST - 1, rdst, rtdst, sub);
             const int mr = sub * 32 + grp * 8 + q;
             const bf16_t* p0 = patch + rt[mr];
             const bf16_t* p1 = patch + rt[mr + 4];
@@ -1488,7 +1507,20 @@ __global__ __launch_bounds__(256) void g3_conv_wgrad_kernel(const GemmDesc* __re
                                                                                      acc[i][gq * JG + jj], 0, 0, 0);
             }
         }
-        st = st + 1 == NST ? 0 : st + 1;
+    };
+    // stage of chunk z + k: k mod NST; the refilled stage is the previous chunk's
+    for (int ch = z; ch < w; ch += NST) {
+        chunk(ch, sm0, rt0, NST == 2 ? sm1 : (NST == 3 ? sm2 : sm3), NST == 2 ? rt1 : (NST == 3 ? rt2 : rt3));
+        if (ch + 1 >= w) break;
+        chunk(ch + 1, sm1, rt1, sm0, rt0);
+        if (NST >= 3) {
+            if (ch + 2 >= w) break;
+            chunk(ch + 2, sm2, rt2, sm1, rt1);
+        }
+        if (NST >= 4) {
+            if (ch + 3 >= w) break;
+            chunk(ch + 3, sm3, rt3, sm2, rt2);
+        }
     }
 
     if (do_bias) {
