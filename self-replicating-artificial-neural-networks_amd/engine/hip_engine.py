@@ -22,6 +22,7 @@ kernels -- no host-driven torch op anywhere in a plan.
 """
 from __future__ import annotations
 
+import os
 import math
 import threading
 import time
@@ -272,6 +273,10 @@ class Launch:
 _NP_TO_TORCH = {np.dtype(np.uint8): torch.uint8, np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
                 np.dtype(np.float32): torch.float32}
 
+
+# Measurement only: launches of these "kind:arg" chunked kinds (e.g. "bn:0,bn:5") are left out of every plan, to
+# bound what fusing them away could save.  The results are wrong with it set; nothing sets it by default.
+_TIMING_SKIP = frozenset(filter(None, os.environ.get("SERANN_TIMING_SKIP", "").split(",")))
 
 class _TableArena:
     """The descriptor and tile tables of one plan, packed into a few device buffers.  A table gets its
@@ -774,7 +779,7 @@ class HipPopulationEngine(PopulationEngine):
                             H.SPLITFIN_ELEMS)
 
         def add_chunked(kind, arg, rows, dtype, counts, chunk):
-            if not rows:
+            if not rows or f"{kind}:{arg}" in _TIMING_SKIP:
                 return
             tiles = H.chunk_tiles(counts, chunk)
             if len(tiles) == 0:

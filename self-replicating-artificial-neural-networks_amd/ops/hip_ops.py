@@ -896,7 +896,9 @@ def dwgrad_ok(geo: dict, M: int, N: int, v: int) -> bool:
         return False
     if int(geo.get("KH", 1)) * int(geo.get("KW", 1)) != 1 or int(geo.get("SH", 1)) * int(geo.get("SW", 1)) != 1:
         return False
-    return int(M) % 8 == 0 and int(N) % 8 == 0 and int(geo.get("C", N)) == int(N)
+    # X rows need only 8-B alignment (C % 4 == 0): a 16-B piece past a row's end carries the next row's first
+    # elements into columns >= N, whose accumulators are never stored
+    return int(M) % 8 == 0 and int(N) % DWGRAD_CALIGN == 0 and int(geo.get("C", N)) == int(N)
 
 
 def wgrad_finalize_row(r: dict, ws_ptr: int, adam: int = 0) -> dict:
@@ -992,6 +994,7 @@ CONV_WGRAD_BNK_MAX = int(_os.environ.get("SERANN_CONV_WGRAD_BNK_MAX", "2048"))
 # C % 8 != 0 and cannot take it; profiles/r5/ab_dma_dense_wgrad.txt)
 DWGRAD = _os.environ.get("SERANN_DWGRAD", "0") != "0"
 DWGRAD_RG = int(_os.environ.get("SERANN_DWGRAD_RG", "2"))
+DWGRAD_CALIGN = int(_os.environ.get("SERANN_DWGRAD_CALIGN", "8"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 

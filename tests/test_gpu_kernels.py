@@ -575,12 +575,14 @@ def test_small_gradients_reach_adam_unquantised():
 
 @pytest.mark.parametrize("F,C,rows,act", [(16, 264, 750, "linear"), (24, 96, 750, "relu"), (64, 64, 20000, "sigmoid"),
                                           (120, 200, 3000, "linear"), (8, 64, 100, "relu"), (40, 128, 75000, "linear"),
-                                          (64, 136, 750, "linear"), (32, 72, 4100, "sigmoid")])
+                                          (64, 136, 750, "linear"), (32, 72, 4100, "sigmoid"),
+                                          (152, 8284, 750, "linear"), (64, 100, 3000, "relu")])
 def test_dma_dense_wgrad(F, C, rows, act, monkeypatch):
     """The LDS-DMA ring Dense WGRAD (gemm3.hip g3_dwgrad_kernel): every (BMF, BNK) instantiation with and without
     the staged Y tile (act' on the A fragments), ragged f / column tiles and 64-row steps, single split (plain
     store) and m-splits (fixed-point atomics); gradient and bias gradient against fp32, bitwise repeatable."""
     monkeypatch.setattr(H, "DWGRAD", True)                  # (off by default: hip_ops.DWGRAD)
+    monkeypatch.setattr(H, "DWGRAD_CALIGN", 4)              # X rows 8-B aligned (C % 4 == 0) allowed
     g = torch.Generator(device=DEV).manual_seed(11)
     x = H.padded(torch.randn(rows, C, device=DEV, generator=g).bfloat16())
     dy = H.padded(torch.randn(rows, F, device=DEV, generator=g).bfloat16())
