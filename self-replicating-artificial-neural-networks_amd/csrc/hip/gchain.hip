@@ -38,6 +38,12 @@
 #include "common.h"
 #include "serann_hip.h"
 
+// dZ2 / dZ1 as bf16 hi + lo pairs in the full backward (round 5): two extra MFMAs per 16 rows for ~16 bits of dZ
+// in dW1 instead of 8 (compile-time: -DGC_HILO=0 builds the single-rounding form for A/B)
+#ifndef GC_HILO
+#define GC_HILO 1
+#endif
+
 #ifndef GC_BWD_MINW
 #define GC_BWD_MINW 2       // waves per SIMD the backward kernels are register-budgeted for
 #endif
@@ -453,7 +459,7 @@ struct GcBwdLds {
     static constexpr int DY = 32 * F2P;                          // staged dy rows [32][F2]
     // MODE 2 stages dy only; MODE 3 also the Z1 / dZ1 / dZ2 images
     // (+ the dZ1 low-part image: dW1 takes dZ1 as hi + lo bf16 pairs, below)
-    static constexpr int PER_WAVE = MODE == 2 ? DY : DY + 3 * 32 * LD1 + 32 * LD2;
+    static constexpr int PER_WAVE = MODE == 2 ? DY : DY + (GC_HILO ? 3 : 2) * 32 * LD1 + 32 * LD2;
     // fp32 reduction slots after the loop (alias the per-wave regions)
     static constexpr int RED = MODE == 2 ? 2 * F2P : F2P * F1P + F1P * 16 + F1P + F2P;
     static constexpr int TOTAL = 4 * PER_WAVE > 2 * RED ? 4 * PER_WAVE : 2 * RED;
@@ -653,7 +659,7 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
                 for (int j = 0; j < 8; ++j) {
                     const float e = dz2[2 * s + (j >> 2)][j & 3];
                     dzb[s].h[j] = gc_bf(e);
-                    dzl[s].h[j] = gc_bf(e - bf2f(dzb[s].h[j]));
+                    if (GC_HILO) dzl[s].h[j] = gc_bf(e - bf2f(dzb[s].h[j]));
                 }
             // images: rows lr, channels 16 mt + 4 q .. + 3 (8-B stores)
 #pragma unroll
@@ -675,7 +681,7 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
             for (int mt = 0; mt < T1; ++mt) {
                 gc_f32x4_t v = gc_f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int s = 0; s < F2K; ++s) v = gc_mma(w2t[mt][s], dzl[s], v);
+                for (int s = 0; s < F2K; ++s) if (GC_HILO) v = gc_mma(w2t[mt][s], dzl[s], v);
 #pragma unroll
                 for (int s = 0; s < F2K; ++s) v = gc_mma(w2t[mt][s], dzb[s], v);
                 if constexpr (A1 != ACT_LINEAR) {
@@ -695,7 +701,7 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
                 *(gc_lu32x2*)(&imgDZ1[lr * LD1 + 16 * mt + 4 * q]) = u;
                 u.x = (uint32_t)lb[0] | ((uint32_t)lb[1] << 16);
                 u.y = (uint32_t)lb[2] | ((uint32_t)lb[3] << 16);
-                *(gc_lu32x2*)(&imgDZ1lo[lr * LD1 + 16 * mt + 4 * q]) = u;
+                if (GC_HILO) *(gc_lu32x2*)(&imgDZ1lo[lr * LD1 + 16 * mt + 4 * q]) = u;
             }
         }
         if (MODE == 2) continue;
@@ -728,8 +734,10 @@ __global__ __launch_bounds__(256, GC_BWD_MINW) void gchain_bwd_kernel(const GCha
         for (int m1 = 0; m1 < T1; ++m1) {
             GcFrag a1, a1l;
             gc_tr_read(a1, imgDZ1, LD1, 16 * m1, lane);
-            gc_tr_read(a1l, imgDZ1lo, LD1, 16 * m1, lane);
-            dw1[m1] = gc_mma(a1l, pp, dw1[m1]);
+            if (GC_HILO) {
+                gc_tr_read(a1l, imgDZ1lo, LD1, 16 * m1, lane);
+                dw1[m1] = gc_mma(a1l, pp, dw1[m1]);
+            }
             dw1[m1] = gc_mma(a1, pp, dw1[m1]);
         }
     }
