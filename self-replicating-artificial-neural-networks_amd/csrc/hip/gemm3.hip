@@ -1084,8 +1084,9 @@ template <int NT, int RT, int PATCH>
 __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __restrict__ descs,
                                                           const int4* __restrict__ tiles) {
     constexpr int TM = 64 * RT, BN = NT * 16;
-    // k-steps per weight chunk: the weight buffers stay near 10 KB with the 64 KB patch tier (two blocks
-    // per CU) and near 17 KB with the smaller tiers
+    // k-steps per weight chunk: the weight buffers stay near 4-5 KB with the 64 KB patch tier (two blocks
+    // per CU: 16-KB weight buffers instead, one block per CU, measured slower -- profiles/r5/ab_conv_fwd_kc.txt)
+    // and near 17 KB with the smaller tiers
     constexpr int KC = (PATCH >= 32768 ? 4 : 8) / NT;
     constexpr int LDBC = KC * 32 + 8;                   // weight row stride: an odd number of 16-B slots
     // the patch region doubles as the output staging tile after the k loop
