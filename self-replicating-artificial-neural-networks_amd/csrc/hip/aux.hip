@@ -120,6 +120,23 @@ __device__ __forceinline__ float wsum(const long long* ws, int C, int idx) {
 // with flags 128 / 256 ONE bias element that receives -/+ the sum over every channel: the Dense(units=1)
 // subtracted from / added to the BN input (x = a - Dense(..)): its bias gradient is -sum(dx), taken here in fp32
 // (the bf16 dx the sub's reduction sees left noise ~1000x torch-bf16's on that mathematically-zero sum).
+// Batch mean and biased variance of channel c from the phase-0 workspace: shifted sums against K = x[0][c] (bn phase 0,
+// the narrow FWD kernel), or with flag 512 unshifted sums accumulated by the producing GEMM's epilogue (GF_BNUSTAT),
+// finished in double
+__device__ __forceinline__ void bn_mu_var(const BnDesc& d, const long long* ws, int C, float Rf, int c, float& mu,
+                                          float& var) {
+    if (d.flags & 512) {
+        const double m = fxw_sum_d<BN_WS_STRIPES>(ws, C, c) / (double)Rf;
+        mu = (float)m;
+        var = (float)fmax(fxw_sum_d<BN_WS_STRIPES>(ws, C, C + c) / (double)Rf - m * m, 0.0);
+    } else {
+        const float K = bf2f(reinterpret_cast<const bf16_t*>(d.x)[c]);
+        const float m1 = wsum(ws, C, c) / Rf;
+        mu = K + m1;
+        var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
+    }
+}
+
 __device__ __forceinline__ int pdb_index(const BnDesc& d, int c) { return (d.flags & (128 | 256)) ? 0 : c; }
 __device__ __forceinline__ float pdb_sign(const BnDesc& d) { return (d.flags & 128) ? -1.f : 1.f; }
 
@@ -201,10 +218,7 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
         } else if (phase == 2 || phase == 3) {
             float mu, var;
             if (phase == 2) {
-                const float K = bf2f(x[c]);
-                const float m1 = wsum(ws, C, c) / Rf;
-                mu = K + m1;
-                var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
+                bn_mu_var(d, ws, C, Rf, c, mu, var);
             } else {
                 mu = reinterpret_cast<const float*>(d.mm)[c];
                 var = reinterpret_cast<const float*>(d.mv)[c];
@@ -235,10 +249,8 @@ __device__ __forceinline__ void bn_vec(const BnDesc& d, int tile, float* sA, flo
         float* mean = reinterpret_cast<float*>(d.mean);
         float* invstd = reinterpret_cast<float*>(d.invstd);
         for (int c = t; c < C; c += 256) {
-            const float K = bf2f(x[c]);
-            const float m1 = wsum(ws, C, c) / Rf;
-            const float mu = K + m1;
-            const float var = fmaxf(wsum(ws, C, C + c) / Rf - m1 * m1, 0.f);
+            float mu, var;
+            bn_mu_var(d, ws, C, Rf, c, mu, var);
             mm[c] = mm[c] * mom + mu * (1.f - mom);
             // BatchNormalizationF16's n / (n - (1 + eps)) (BatchNormalizationF16.py:134-140); flag 64: the
             // plain Bessel factor n / (n - 1) of a standard BatchNormalization (the RiboAE's)

@@ -106,6 +106,18 @@ __device__ __forceinline__ float fxw_sum(const long long* ws, int C, int idx) {
     }
     return (float)((double)hi + (double)lo * (1.0 / 4294967296.0));
 }
+// The same sum in double (unshifted statistics: sum x^2 - (sum x)^2 / n without fp32 cancellation)
+template <int STRIPES>
+__device__ __forceinline__ double fxw_sum_d(const long long* ws, int C, int idx) {
+    long long hi = 0;
+    u64_t lo = 0;
+#pragma unroll
+    for (int s = 0; s < STRIPES; ++s) {
+        hi += ws[2 * (s * 2 * C + idx)];
+        lo += (u64_t)ws[2 * (s * 2 * C + idx) + 1];
+    }
+    return (double)hi + (double)lo * (1.0 / 4294967296.0);
+}
 
 // Keras / TF ResourceApplyAdam on one element (experiment_worker.py:80): shared by the arena-wide Adam pass
 // and the WGRAD epilogues that apply the step to their own tile (GF_ADAM), so both give the same bits.

@@ -301,6 +301,60 @@ __device__ __forceinline__ void wave_store_rows(bf16_t* __restrict__ st, bf16_t*
 
 }  // namespace
 
+
+// GF_BNUSTAT (FWD epilogues of the conv-halo, direct and LDS-tiled kernels): this output feeds a BatchNormalization
+// -- accumulate its phase-0 statistics here, unshifted (K = 0: sum x and sum x^2 of the stored bf16 values; the BN's
+// flag 512 makes phase 2 finish them in double, where the integer-exact sums lose nothing to cancellation).  A
+// wave's rows of each accumulator column are summed in fp32 in a fixed order, the waves' partials meet in LDS in
+// wave order, and the block adds them to its stripe of the wide fixed-point workspace d.aux: one atomic pair per
+// column and sum per block (deterministic).  The block's 4 waves cover WG column groups of NT * 16 columns (wave w:
+// group w % WG, at column colblk + (w % WG) * NT * 16); red holds 4 x 2 x WG * NT * 16 floats.  Contains a barrier:
+// every thread of the block calls it.
+template <int RT, int NT, int WG, typename RowOk>
+__device__ __forceinline__ void bn_ustat_flush(const GemmDesc& d, const f32x4_t (&acc)[RT][NT], RowOk row_ok,
+                                               int colblk, int ncols, const float* __restrict__ bias, int act,
+                                               float* red, int wave, int lane, int C) {
+    constexpr int WC = NT * 16, BC = WG * WC;
+    const int r16 = lane & 15, rq = (lane >> 4) * 4;
+    const int coff = (wave % WG) * WC;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int col = colblk + coff + j * 16 + r16;
+        const float bv = (bias && col < ncols) ? bias[col] : 0.f;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (row_ok(i, rq + r)) {
+                    const float v = bf2f(f2bf(apply_act(acc[i][j][r] + bv, act)));
+                    s1 += v;
+                    s2 += v * v;
+                }
+            }
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (lane < 16) {
+            red[(wave * 2 + 0) * BC + coff + j * 16 + lane] = s1;
+            red[(wave * 2 + 1) * BC + coff + j * 16 + lane] = s2;
+        }
+    }
+    __syncthreads();
+    long long* ws = reinterpret_cast<long long*>(d.aux) + (blockIdx.x % BN_WS_STRIPES) * 4 * C;
+    for (int e = threadIdx.x; e < 2 * BC; e += blockDim.x) {
+        const int which = e / BC, cl = e - which * BC;
+        const int col = colblk + cl;
+        if (col >= ncols) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (w % WG == cl / WC) v += red[(w * 2 + which) * BC + cl];
+        fxw_add(ws + 2 * (which * C + col), v);
+    }
+}
+
 // ==================================================================================================
 // FWD / DGRAD direct-fragment kernel.  NT = BN/16 column tiles, RT = 16-row tiles per wave.
 //   KW = false: block = 4 waves x RT*16 rows; every wave runs the whole k range.
@@ -506,6 +560,13 @@ void g3_direct_kernel(const GemmDesc* __restrict__ descs,
 
     // epilogue: one contiguous output range per wave when the block spans all N columns
     const float* bias = reinterpret_cast<const float*>(d.bias);
+    if constexpr (MODE == MODE_FWD && !KW) {
+        if (g.flags & GF_BNUSTAT) {
+            __shared__ float bnred[4 * 2 * BNB];
+            bn_ustat_flush<RT, NT, 1>(d, acc, [&](int i, int rr) { return m_w + i * 16 + rr < g.M; }, n0, g.N, bias,
+                                      g.act, bnred, wave, lane, g.N);
+        }
+    }
     if (n0 == 0 && g.N <= BNB && !(g.flags & GF_OUT_F32)) {
         const int nrows = min(WROWS, g.M - m_w);
         if (nrows > 0) {
@@ -1215,6 +1276,11 @@ __global__ __launch_bounds__(256) void g3_conv_fwd_kernel(const GemmDesc* __rest
     const float* bias = reinterpret_cast<const float*>(d.bias);
     bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
     const int64_t rowbase = (int64_t)b * ohw;
+    if (g.flags & GF_BNUSTAT) {
+        __shared__ float bnred[4 * 2 * BN];
+        bn_ustat_flush<RT, NT, 1>(d, acc, [&](int i, int rr) { return m0 + (wave * RT + i) * 16 + rr <= m_last; },
+                                  n0, g.N, bias, g.act, bnred, wave, lane, g.N);
+    }
     if (n0 == 0 && g.N <= BN && !(g.flags & GF_OUT_F32)) {
         // the block's rows are consecutive pixels of one image: contiguous output rows
         const int mw = m0 + wave * RT * 16;
@@ -2258,6 +2324,14 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     const float* bias = (MODE == MODE_FWD) ? reinterpret_cast<const float*>(d.bias) : nullptr;
     const int oact = (MODE == MODE_FWD) ? act : ACT_LINEAR;
     const int rq = (lane >> 4) * 4;
+    if constexpr (MODE == MODE_FWD) {
+        if (flags & GF_BNUSTAT) {                    // (never with GF_SPLITWS: the planner's condition)
+            float* bnred = reinterpret_cast<float*>(lds);        // the k loop ended on a barrier
+            bn_ustat_flush<4, NTW, 2>(d, acc, [&](int i, int rr) { return m0 + wr * 64 + i * 16 + rr < M; }, n0, N,
+                                      bias, act, bnred, wave, lane, N);
+            __syncthreads();                         // (the staging epilogue below reuses the LDS)
+        }
+    }
     if constexpr (MODE == MODE_DGRAD && NS) {
         // NS (GF_NBNSUM; its own instantiation, so the other DGRADs keep their registers / occupancy).
         // This DGRAD produces dY of a fused raw-input Dense -> BatchNormalization pair with ONE input channel

@@ -42,6 +42,8 @@ enum GemmFlags : int64_t {
                           // epilogue instead of storing the gradient; the arena-wide Adam pass skips it
     GF_NOSTORE = 32,      // FWD narrow kernel with GF_BNSTAT: statistics only, the output is never stored
                           // (its only consumer recomputes it: nbn.hip)
+    GF_BNUSTAT = 1024,    // FWD (conv-halo, direct non-KW, LDS-tiled without k splits): also accumulate the consuming
+                          // BatchNorm's phase-0 statistics, unshifted, into aux (its workspace; BnDesc flag 512)
     GF_NBNSUM = 512,      // DGRAD (LDS-tiled kernel) producing the output gradient of a fused raw-input
                           // Dense (1 input channel) -> BN pair (ext = its NbnDesc): instead of storing dY, reduce the BN / Dense
                           // backward sums of every column over the block's rows into NbnDesc::part; nbn
@@ -108,6 +110,7 @@ struct BnDesc {
                               // bf16-rounded dZ over ~600k rows instead leaves O(sqrt(R) * 2^-9) noise.
                               // flags 128 / 256: pdb is ONE bias element that receives -/+ sum(dx) over all
                               // channels (a Dense(units=1) subtracted from / added to the BN input)
+                              // flag 512: ws holds unshifted phase-0 sums from the producer (GF_BNUSTAT)
     double eps, momentum;
 };
 struct PoolDesc { int64_t x, y, idx, dy, dx, B, H, W, C, OH, OW, PH, PW, SH, SW, flags; };  // flags: 1 accum

@@ -44,6 +44,8 @@ import os
 ALIGN = 16  # elements; keeps every buffer 32-B aligned for bf16 and 64-B for fp32
 SLACK = 64  # elements of zeroed tail on every arena
 FUSE_BN_STATS = os.environ.get("SERANN_FUSE_BN_STATS", "1") != "0"
+# BN phase-0 statistics in the producing conv-halo / direct / LDS-tiled FWD epilogue (GF_BNUSTAT, round 5)
+FUSE_BN_USTATS = os.environ.get("SERANN_FUSE_BN_USTATS", "1") != "0"
 FUSE_CONVPOOL = os.environ.get("SERANN_FUSE_CONVPOOL", "1") != "0"
 FUSE_GCHAIN = os.environ.get("SERANN_FUSE_GCHAIN", "1") != "0"
 
@@ -1019,6 +1021,20 @@ class HipPopulationEngine(PopulationEngine):
                 S += ns
             return out, S
 
+        bn_ustat = set()
+
+        def bnustat(o, n, row, M, F, K):
+            """The FWD row of a GEMM whose output feeds a BatchNormalization accumulates that BN's phase-0 statistics
+            (unshifted) in its epilogue when its kernel can (hip_ops.fwd_bnustat_ok); the BN's phase-0 launch is
+            dropped and its phase 2 reads the sums with BnDesc flag 512."""
+            bnc = bn_consumer[o].get(n.id)
+            if not (train and bnc is not None and FUSE_BN_USTATS and F <= 256 and H.fwd_bnustat_ok(row, M, F, K)):
+                return
+            row["aux"] = mem["ws"].ptr(mem["orgs"][o]["bn"][bnc]["ws"])
+            row["flags"] |= H.GF_BNUSTAT
+            bn_prefused.add((o, bnc))
+            bn_ustat.add((o, bnc))
+
         # ---- forward ---------------------------------------------------------------------------
         for d in range(1, maxd + 1):
             fin_rows = []
@@ -1089,6 +1105,7 @@ class HipPopulationEngine(PopulationEngine):
                             g_rows.append(dict(a=ic["buf"].data_ptr(), b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=OH,
                                                W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=F,
                                                K=K, act=act, flags=flags))
+                            bnustat(o, n, g_rows[-1], M, F, K)
                         else:
                             g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,
                                                OW=OW, F=F, KH=KH, KW=KW, SH=SH, SW=SW, M=M, N=F, K=K, act=act,
@@ -1106,6 +1123,8 @@ class HipPopulationEngine(PopulationEngine):
                             elif n.id in nbn_src[o]:
                                 raise RuntimeError(f"organism {o}: Dense {n.id} fused with its BatchNormalization "
                                                    f"but not on the narrow statistics kernel")
+                            else:
+                                bnustat(o, n, g_rows[-1], M, F, K)
                         if n.id not in fcons[o]:
                             g_dims.append((M, F, K))      # (K slices appended their own dims)
                     elif n.op == "pool":
@@ -1120,6 +1139,8 @@ class HipPopulationEngine(PopulationEngine):
                         bd = rec["bn"][n.id]
                         c = a["channels"]
                         flags = (1 if n.id in lay.gamma else 0) | (2 if n.id in lay.beta else 0)
+                        if (o, n.id) in bn_ustat:
+                            flags |= H.BN_USTAT
                         bn_rows.append(dict(x=self._act_ptr(mem, o, n.inputs[0], inputs),
                                             y=self._act_ptr(mem, o, n.id, inputs),
                                             gamma=pptr(lay.gamma[n.id]) if n.id in lay.gamma else 0,

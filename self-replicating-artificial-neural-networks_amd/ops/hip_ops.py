@@ -53,6 +53,8 @@ LOSS_DTYPE = np.dtype([(f, _I) for f in ["logits", "dlogits", "labels", "target"
                       + [("lb", np.float64)])
 
 GF_VEC_A, GF_VEC_B, GF_ACCUM, GF_OUT_F32, GF_WSTORE, GF_SPLITWS, GF_BNSTAT = 1, 2, 4, 8, 16, 64, 128
+GF_BNUSTAT = 1024      # FWD epilogue accumulates the consuming BN's unshifted phase-0 sums (BnDesc flag BN_USTAT)
+BN_USTAT = 512
 GF_NBNSUM = 512
 GF_NOSTORE = 32
 GF_ADAM = 256
@@ -887,6 +889,24 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000)
         out.append((v, [r for r, _ in items], tiles))
     return out
+
+
+def fwd_bnustat_ok(r: dict, M: int, N: int, K: int, splitk: bool = True) -> bool:
+    """True when the FWD kernel gemm3_plan picks for row ``r`` accumulates a consuming BatchNorm's statistics in its
+    epilogue (GF_BNUSTAT): the conv-halo kernel, the LDS-tiled kernel without k splits, or the direct kernel without
+    the wave-split-K form -- mirrors gemm3_plan's selection (narrow rows have their own GF_BNSTAT)."""
+    flags = int(r.get("flags", 0))
+    if flags & (GF_ACCUM | GF_OUT_F32 | GF_SPLITWS) or r.get("_force_tiled") or r.get("_split"):
+        return False
+    if narrow_k(r, MODE_FWD, M, N, K) is not None and not r.get("_nonarrow"):
+        return False
+    one = int(r.get("KH", 1)) * int(r.get("KW", 1)) == 1 and int(r.get("SH", 1)) * int(r.get("SW", 1)) == 1
+    if "tiled" not in _OFF and K > 32 and one:
+        return not (splitk and tiled_fwd_splits(M, N, K, tiled_bn(N), flags) > 1)
+    if conv_lds_config(r, N) is not None:
+        return True
+    v = gemm3_variant(MODE_FWD, M, N, K, r)
+    return v >= 5000 or (v % 1000) < 100          # single-step, or the direct kernel without wave-split K
 
 
 def dwgrad_ok(geo: dict, M: int, N: int, v: int) -> bool:

@@ -24,6 +24,7 @@ Descriptors, tile tables and every activation / gradient buffer are built once p
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -60,6 +61,7 @@ class HipRiboTrainer:
         self.dev = torch.device(device)
         self.b1, self.b2, self.eps = beta1, beta2, eps
         self.ksplit = int(ksplit)                 # k splits of the 229,824-wide Dense FWD (>= 256 blocks at B=512)
+        self.fuse_bn_stats = os.environ.get("SERANN_FUSE_BN_USTATS", "1") != "0"
         self.lib = H.lib(required=True)
         H.check_layouts()
         inf, gen = model.inference_net, model.generative_net
@@ -286,10 +288,17 @@ class HipRiboTrainer:
             K = g_["KH"] * g_["KW"] * g_["C"]
             geo = dict(g_, SH=1, SW=1)
             vec = (H.GF_VEC_A if g_["C"] % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)
-            fwd += self._gemm(H.MODE_FWD, [dict(a=P(prev), b=self.bptr(name), out=P(name), bias=self.pptr(name + "_b"),
-                                                M=M, N=g_["F"], K=K, act=0, flags=vec, **geo)], [(M, g_["F"], K)])
+            frow = dict(a=P(prev), b=self.bptr(name), out=P(name), bias=self.pptr(name + "_b"),
+                        M=M, N=g_["F"], K=K, act=0, flags=vec, **geo)
             bf_, bb_ = self._bn_row(bname, P(name), P("y" + name), P("d" + name), P("dz" + name), M)
-            fwd += [self._bn_launch(0, bf_), self._bn_launch(2, bf_)]
+            # the conv's FWD epilogue accumulates the BN's statistics (GF_BNUSTAT): no phase-0 pass over its output
+            ustat = self.fuse_bn_stats and g_["F"] <= 256 and H.fwd_bnustat_ok(frow, M, g_["F"], K, splitk=False)
+            if ustat:
+                frow.update(aux=self.buf["ws"].data_ptr() + 8 * self.wsa.items[bname][0],
+                            flags=vec | H.GF_BNUSTAT)
+                bf_["flags"] |= H.BN_USTAT
+            fwd += self._gemm(H.MODE_FWD, [frow], [(M, g_["F"], K)])
+            fwd += ([] if ustat else [self._bn_launch(0, bf_)]) + [self._bn_launch(2, bf_)]
             # backward of this block (appended in reverse below)
             blk = [self._bn_launch(4, bb_), self._bn_launch(5, bb_)]
             blk += self._gemm(H.MODE_WGRAD, [dict(a=P("dz" + name), b=P(prev), out=self.gptr(name),
@@ -330,11 +339,16 @@ class HipRiboTrainer:
         g1 = self.geo["g1"]
         M1, K1 = B * g1["OH"], g1["KH"] * g1["C"]
         geo1 = dict(g1, SH=1, SW=1)
-        dec += self._gemm(H.MODE_FWD, [dict(a=P("zb"), b=self.bptr("g1"), out=P("h1"), bias=self.pptr("g1_b"),
-                                            M=M1, N=g1["F"], K=K1, act=0, flags=H.GF_VEC_B if K1 % 8 == 0 else 0, **geo1)],
-                          [(M1, g1["F"], K1)])
+        g1row = dict(a=P("zb"), b=self.bptr("g1"), out=P("h1"), bias=self.pptr("g1_b"),
+                     M=M1, N=g1["F"], K=K1, act=0, flags=H.GF_VEC_B if K1 % 8 == 0 else 0, **geo1)
         gb1f, gb1b = self._bn_row("gbn1", P("h1"), P("yh1"), P("dh1"), P("dzh1"), M1)
-        dec += [self._bn_launch(0, gb1f), self._bn_launch(2, gb1f)]
+        ustat = self.fuse_bn_stats and g1["F"] <= 256 and H.fwd_bnustat_ok(g1row, M1, g1["F"], K1, splitk=False)
+        if ustat:
+            g1row.update(aux=self.buf["ws"].data_ptr() + 8 * self.wsa.items["gbn1"][0],
+                         flags=g1row["flags"] | H.GF_BNUSTAT)
+            gb1f["flags"] |= H.BN_USTAT
+        dec += self._gemm(H.MODE_FWD, [g1row], [(M1, g1["F"], K1)])
+        dec += ([] if ustat else [self._bn_launch(0, gb1f)]) + [self._bn_launch(2, gb1f)]
         K2, N2 = self.gflat, L * V
         dec += self._gemm(H.MODE_FWD, [dict(a=P("yh1"), b=self.bptr("g2"), out=P("h2"), bias=self.pptr("g2_b"),
                                             C=K2, F=N2, M=B, N=N2, K=K2, act=0, flags=H.GF_VEC_A | H.GF_VEC_B,

@@ -609,3 +609,41 @@ def test_dma_dense_wgrad(F, C, rows, act, monkeypatch):
     ref = dz.double().t() @ x.double()
     assert _rel(_q(res[0][0]), ref.float()) < 2e-5
     assert _rel(_q(res[0][1]), dz.double().sum(0).float()) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [
+    (4, 12, 12, 16, 32, 3, 3, "relu"),        # conv-halo FWD
+    (3, 9, 7, 64, 24, 1, 1, "sigmoid"),       # 1x1, K = 64: LDS-tiled FWD
+    (5, 6, 6, 16, 40, 1, 1, "linear"),        # 1x1, K = 16: single-step direct FWD
+    (2, 13, 13, 13, 20, 3, 3, "linear"),      # odd channels, conv-halo
+    (6, 10, 10, 8, 70, 3, 3, "relu"),         # several column tiles
+])
+def test_fwd_epilogue_bn_statistics(shape):
+    """GF_BNUSTAT: the FWD epilogue (conv-halo, LDS-tiled, direct kernels) accumulates sum y and sum y^2 of its stored
+    bf16 outputs per channel into a BatchNorm statistics workspace (wide fixed point, BN_WS_STRIPES copies) -- what
+    BN phase 2 reads with flag 512 -- and the output itself is unchanged."""
+    B, Hh, Ww, C, Fo, KH, KW, act = shape
+    OH, OW = Hh - KH + 1, Ww - KW + 1
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV, generator=g).bfloat16())
+    w = H.padded((torch.randn(Fo, KH, KW, C, device=DEV, generator=g) / math.sqrt(KH * KW * C)).bfloat16())
+    bias = H.padded(torch.randn(Fo, device=DEV, generator=g) + 2.0)      # |mean| >> std: no cancellation either
+    M, K = B * OH * OW, KH * KW * C
+    geo = dict(H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=Fo, KH=KH, KW=KW, SH=1, SW=1)
+    flags = (H.GF_VEC_A if C % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0)
+    row = dict(a=x.data_ptr(), b=w.data_ptr(), bias=bias.data_ptr(), M=M, N=Fo, K=K, act=H.ACT_CODES[act], **geo)
+    assert H.fwd_bnustat_ok(dict(row, flags=flags), M, Fo, K)
+    outs = []
+    for extra in (0, H.GF_BNUSTAT):
+        y = H.padded(torch.zeros(B, OH, OW, Fo, dtype=torch.bfloat16, device=DEV))
+        ws = H.operand(H.bn_ws_words(Fo), torch.int64, DEV)
+        ws.zero_()
+        _run_gemm(H.MODE_FWD, [dict(row, out=y.data_ptr(), aux=ws.data_ptr() if extra else 0, flags=flags | extra)],
+                  [(M, Fo, K)])
+        outs.append((y.clone(), ws.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    yv = outs[1][0].double().reshape(M, Fo)
+    w4 = outs[1][1][:H.bn_ws_words(Fo)].reshape(H.BN_WS_STRIPES, 2 * Fo, 2).cpu()
+    sums = (w4[..., 0].double() + w4[..., 1].double() / 2.0 ** 32).sum(0)
+    torch.testing.assert_close(sums[:Fo], yv.sum(0).cpu(), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(sums[Fo:], (yv * yv).sum(0).cpu(), rtol=1e-5, atol=1e-3)
