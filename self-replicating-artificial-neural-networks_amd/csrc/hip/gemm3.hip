@@ -616,7 +616,7 @@ __device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only 
 // Q40 store (sole writer) or fixed-point atomics (m-split).
 template <int TF, int TK>
 __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x4_t (&acc)[TF][TK], int frow0,
-                                            int kcol0, int lane) {
+                                            int kcol0, int lane, float* stage = nullptr, int wave = 0) {
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
@@ -630,6 +630,61 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
         float* __restrict__ Vo = reinterpret_cast<float*>(ac.v);
         bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
         const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+        if (stage != nullptr) {
+            // Row-major through LDS (stage: 2 x TR x LD floats; the k loop's tiles are dead): a lane of the
+            // accumulator layout holds 4 rows x 1 column of each 16 x 16 tile, so updating in place read and wrote
+            // p / m / v / pbf as 64-B quarter rows, one element per lane per instruction.  Staged, a lane takes 4
+            // consecutive columns of one row: 16-B accesses, whole 256-B row segments per 16 lanes, a quarter of the
+            // memory instructions.  Two rounds of two waves (the LDS holds two wave tiles).
+            constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG;
+            const int64_t t0 = e0 + (int64_t)frow0 * ldo + kcol0;
+            const bool vec = (t0 & 3) == 0 && (ldo & 3) == 0;      // float4-aligned rows
+            const int cg = lane % CG, rr = lane / CG;
+            for (int half = 0; half < 2; ++half) {
+                __syncthreads();
+                if ((wave >> 1) == half) {
+                    float* st = stage + (wave & 1) * TR * LD;
+#pragma unroll
+                    for (int i = 0; i < TF; ++i)
+#pragma unroll
+                        for (int j = 0; j < TK; ++j)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) st[(i * 16 + rq + r) * LD + j * 16 + c16] = acc[i][j][r];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (int r0 = 0; r0 < TR; r0 += RPI) {
+                        const int row = frow0 + r0 + rr, col = kcol0 + cg * 4;
+                        if (row >= g.M || col >= g.N) continue;
+                        const float4 gv = *reinterpret_cast<const float4*>(&st[(r0 + rr) * LD + cg * 4]);
+                        const int64_t e = e0 + (int64_t)row * ldo + col;
+                        if (vec && col + 4 <= g.N) {
+                            float4 p4 = *reinterpret_cast<const float4*>(&P[e]);
+                            float4 m4 = *reinterpret_cast<const float4*>(&Mo[e]);
+                            float4 v4 = *reinterpret_cast<const float4*>(&Vo[e]);
+                            adam_elem(p4.x, m4.x, v4.x, fx_f(fx_q(gv.x)), lr_t, ac.b1, ac.b2, ac.eps);
+                            adam_elem(p4.y, m4.y, v4.y, fx_f(fx_q(gv.y)), lr_t, ac.b1, ac.b2, ac.eps);
+                            adam_elem(p4.z, m4.z, v4.z, fx_f(fx_q(gv.z)), lr_t, ac.b1, ac.b2, ac.eps);
+                            adam_elem(p4.w, m4.w, v4.w, fx_f(fx_q(gv.w)), lr_t, ac.b1, ac.b2, ac.eps);
+                            *reinterpret_cast<float4*>(&P[e]) = p4;
+                            *reinterpret_cast<float4*>(&Mo[e]) = m4;
+                            *reinterpret_cast<float4*>(&Vo[e]) = v4;
+                            *reinterpret_cast<uint2*>(&Pb[e]) = make_uint2(f2bf2(p4.x, p4.y), f2bf2(p4.z, p4.w));
+                        } else {
+                            const float gq[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                if (col + q >= g.N) break;
+                                float p_ = P[e + q], m_ = Mo[e + q], v_ = Vo[e + q];
+                                adam_elem(p_, m_, v_, fx_f(fx_q(gq[q])), lr_t, ac.b1, ac.b2, ac.eps);
+                                P[e + q] = p_; Mo[e + q] = m_; Vo[e + q] = v_; Pb[e + q] = f2bf(p_);
+                            }
+                        }
+                    }
+                }
+            }
+            return;
+        }
         // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
         // and stored -- element by element, each load waited behind the previous element's stores (the
         // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
@@ -960,7 +1015,10 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
                 if (j < a_nv) fx_add(dbias + f0 + a_f + j, bsum[j]);
         }
     }
-    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane);
+    // (the fused-Adam epilogue stages through the LDS tiles when two wave tiles of fp32 fit in them)
+    constexpr bool ADAM_STAGE = RG == 1 && NWV == 4 && 2 * (TF * 16) * (TK * 16 + 4) * 4 <= SMEM * 2;
+    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane,
+                        ADAM_STAGE ? reinterpret_cast<float*>(smem) : nullptr, wave);
 }
 
 // ==================================================================================================
