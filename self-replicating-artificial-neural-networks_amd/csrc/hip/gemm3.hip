@@ -723,6 +723,45 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
         }
         return;
     }
+    if (stage != nullptr && (g.flags & GF_WSTORE)) {
+        // sole writer, plain stores: row-major through LDS as the Adam path above, a lane storing 4 consecutive
+        // Q40 elements of a row (two 16-B stores) instead of one 8-B element of 4 rows x 1 column
+        constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG;
+        const bool vec = (reinterpret_cast<uintptr_t>(out + (int64_t)frow0 * ldo + kcol0) & 15) == 0 && (ldo & 1) == 0;
+        const int cg = lane % CG, rr = lane / CG;
+        for (int half = 0; half < 2; ++half) {
+            __syncthreads();
+            if ((wave >> 1) == half) {
+                float* st = stage + (wave & 1) * TR * LD;
+#pragma unroll
+                for (int i = 0; i < TF; ++i)
+#pragma unroll
+                    for (int j = 0; j < TK; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) st[(i * 16 + rq + r) * LD + j * 16 + c16] = acc[i][j][r];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int r0 = 0; r0 < TR; r0 += RPI) {
+                    const int row = frow0 + r0 + rr, col = kcol0 + cg * 4;
+                    if (row >= g.M || col >= g.N) continue;
+                    const float4 gv = *reinterpret_cast<const float4*>(&st[(r0 + rr) * LD + cg * 4]);
+                    long long* o = out + (int64_t)row * ldo + col;
+                    if (vec && col + 4 <= g.N) {
+                        typedef long long ll2 __attribute__((ext_vector_type(2)));
+                        *reinterpret_cast<ll2*>(o) = ll2{fx_q(gv.x), fx_q(gv.y)};
+                        *reinterpret_cast<ll2*>(o + 2) = ll2{fx_q(gv.z), fx_q(gv.w)};
+                    } else {
+                        const float gq[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (col + q < g.N) o[q] = fx_q(gq[q]);
+                    }
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < TF; ++i)
 #pragma unroll

@@ -62,6 +62,10 @@ class HipRiboTrainer:
         self.b1, self.b2, self.eps = beta1, beta2, eps
         self.ksplit = int(ksplit)                 # k splits of the 229,824-wide Dense FWD (>= 256 blocks at B=512)
         self.fuse_bn_stats = os.environ.get("SERANN_FUSE_BN_USTATS", "1") != "0"
+        # the large single-split Dense WGRADs apply Adam in their epilogue (SERANN_FUSE_ADAM=0: the arena pass)
+        self.fuse_adam = os.environ.get("SERANN_FUSE_ADAM", "1") != "0"
+        self.fused_adam = False
+        self.adam_regions: List[tuple] = []
         self.lib = H.lib(required=True)
         H.check_layouts()
         inf, gen = model.inference_net, model.generative_net
@@ -70,17 +74,24 @@ class HipRiboTrainer:
         self.plans: Dict[int, _Plan] = {}
         self.keep: List[torch.Tensor] = []          # split-WGRAD slabs referenced by the launch descriptors
 
-    def _plan(self, B: int) -> _Plan:
-        if B not in self.plans:
+    def _plan(self, B: int, fused: bool = False) -> _Plan:
+        """Buffers and launches of one batch size; ``fused``: single-split WGRAD tiles apply Adam in their epilogue
+        (GF_ADAM) and the arena pass skips them -- the training step's plan.  The unfused plan keeps every gradient
+        in the arena (debug_grads / update=False)."""
+        key = (int(B), bool(fused))
+        if key not in self.plans:
             self.B = int(B)
+            self.fused_adam = bool(fused) and self.fuse_adam
+            self.adam_regions = []
             self._build_buffers()
             self._build_launches()
             pl = _Plan()
             for k in ("buf", "wsa", "mean", "invstd", "fwd_enc", "fwd_dec", "bwd_dec", "bwd_enc", "trans", "wt"):
                 setattr(pl, k, getattr(self, k))
             pl.B = int(B)
-            self.plans[B] = pl
-        return self.plans[B]
+            pl.skip = H.adam_skip_mask_device(self.pa.size, self.adam_regions, self.dev) if self.adam_regions else None
+            self.plans[key] = pl
+        return self.plans[key]
 
     # ------------------------------------------------------------------------------------------------
     # parameter arena: fp32 master, Q40 int64 gradients, Adam moments, bf16 compute copy
@@ -119,6 +130,10 @@ class HipRiboTrainer:
         self.stats = _zeros(sa.size, torch.float32, dev)
         self.step_i = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        actx = np.zeros(1, dtype=H.ADAM_CTX_DTYPE)
+        actx[0] = (self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(), self.g.data_ptr(),
+                   self.lr_t.data_ptr(), self.b1, self.b2, self.eps, 0.0)
+        self._adam_ctx = torch.as_tensor(np.frombuffer(actx.tobytes(), dtype=np.uint8).copy(), device=dev)
         with torch.no_grad():
             for name, mod, attr, klayout, perm in self.specs:
                 off, cnt = pa.items[name]
@@ -241,6 +256,11 @@ class HipRiboTrainer:
                     ws = _zeros(H.wgrad_slab_elems(r), torch.float32, self.dev)
                     self.keep.append(ws)
                     fin.append(H.wgrad_finalize_row(r, ws.data_ptr()))
+            if mode == H.MODE_WGRAD:
+                for r in rws:
+                    if int(r.get("flags", 0)) & H.GF_ADAM:
+                        self.adam_regions.append(((int(r["out"]) - self.g.data_ptr()) // 8, int(r["M"]), int(r["N"]),
+                                                  int(r.get("ldo") or r["N"])))
             clean = [{k: val for k, val in r.items() if not k.startswith("_")} for r in rws]
             d = torch.as_tensor(np.frombuffer(H.gemm_desc_array(clean).tobytes(), dtype=np.uint8).copy(), device=self.dev)
             out.append(("gemm3", (mode, v), d, torch.as_tensor(np.ascontiguousarray(tiles), device=self.dev)))
@@ -358,13 +378,15 @@ class HipRiboTrainer:
         self.fwd_dec = dec
         # --- decoder backward ----------------------------------------------------------------------
         db = [self._bn_launch(4, gb2b), self._bn_launch(5, gb2b)]
-        db += self._gemm(H.MODE_WGRAD, [dict(a=P("dzh2"), b=P("yh1"), out=self.gptr("g2"), bias=self.gptr("g2_b"),
-                                             aux=0, act=0, C=K2, F=N2, M=N2, N=K2, K=B,
-                                             flags=H.GF_VEC_A | (H.GF_VEC_B if K2 % 8 == 0 else 0),
-                                             **dense_geo)], [(N2, K2, B)])
+        # (DGRAD first: with fused Adam the WGRAD epilogue updates the weights the DGRAD reads)
         db += self._gemm(H.MODE_DGRAD, [dict(a=P("dzh2"), b=0, _bnat=self.bptr("g2"), aux=0, act=0, out=P("dh1"),
                                              C=K2, F=N2, M=B, N=K2, K=N2, flags=H.GF_VEC_A | H.GF_VEC_B,
                                              **dense_geo)], [(B, K2, N2)])
+        db += self._gemm(H.MODE_WGRAD, [dict(a=P("dzh2"), b=P("yh1"), out=self.gptr("g2"), bias=self.gptr("g2_b"),
+                                             adam=self._adam_ctx.data_ptr() if self.fused_adam else 0,
+                                             aux=0, act=0, C=K2, F=N2, M=N2, N=K2, K=B,
+                                             flags=H.GF_VEC_A | (H.GF_VEC_B if K2 % 8 == 0 else 0),
+                                             **dense_geo)], [(N2, K2, B)])
         db += [self._bn_launch(4, gb1b), self._bn_launch(5, gb1b)]
         db += self._gemm(H.MODE_WGRAD, [dict(a=P("dzh1"), b=P("zb"), out=self.gptr("g1"), bias=self.gptr("g1_b"),
                                              aux=0, act=0, M=g1["F"], N=K1, K=M1,
@@ -377,14 +399,16 @@ class HipRiboTrainer:
         self.bwd_dec = db
         # --- encoder backward (after the concrete backward) ----------------------------------------
         eb = []
-        eb += self._gemm(H.MODE_WGRAD, [dict(a=P("dlogitsb"), b=P("yc3"), out=self.gptr("dense"),
-                                             bias=self.gptr("dense_b"), aux=0, act=0, C=K, F=N, M=N, N=K, K=B,
-                                             flags=(H.GF_VEC_A if N % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0),
-                                             **dense_geo)], [(N, K, B)])
+        # (DGRAD first: with fused Adam the WGRAD epilogue updates the weights the DGRAD reads)
         eb += self._gemm(H.MODE_DGRAD, [dict(a=P("dlogitsb"), b=0, _bnat=self.bptr("dense"), aux=0, act=0,
                                              out=P("dc3"), C=K, F=N, M=B, N=K, K=N,
                                              flags=(H.GF_VEC_A if N % 8 == 0 else 0) | H.GF_VEC_B, **dense_geo)],
                          [(B, K, N)])
+        actx = self._adam_ctx.data_ptr() if self.fused_adam else 0
+        eb += self._gemm(H.MODE_WGRAD, [dict(a=P("dlogitsb"), b=P("yc3"), out=self.gptr("dense"), adam=actx,
+                                             bias=self.gptr("dense_b"), aux=0, act=0, C=K, F=N, M=N, N=K, K=B,
+                                             flags=(H.GF_VEC_A if N % 8 == 0 else 0) | (H.GF_VEC_B if K % 8 == 0 else 0),
+                                             **dense_geo)], [(N, K, B)])
         for blk in reversed(enc_bwd):
             eb += blk
         eb += [self._bn_launch(4, bn0b), self._bn_launch(5, bn0b)]
@@ -432,9 +456,12 @@ class HipRiboTrainer:
         L, E, G, A, V = self.L, self.E, self.G, self.A, self.V
         if tuple(tokens.shape) != (B, L):
             raise ValueError(f"expected a (B, {L}) token batch, got {tuple(tokens.shape)}")
-        pl = self._plan(B)
+        pl = self._plan(B, fused=update)
         tp = float(prior_temperature if prior_temperature is not None else self.model.prior_temperature)
         lib, s = self.lib, H.stream_handle()
+        if update and pl.skip is not None:
+            # step counter and lr_t first: the fused-Adam WGRAD epilogues read lr_t during the backward
+            lib.adam_scalars(self.step_i.data_ptr(), self.lr_t.data_ptr(), float(lr), self.b1, self.b2, s)
         buf = pl.buf
         tok = tokens.to(self.dev)
         buf["tok"][:B * L].copy_(tok.reshape(-1))
@@ -475,7 +502,11 @@ class HipRiboTrainer:
                          buf["dlogits"].data_ptr(), B, G, A, float(temperature), tp, s)
         buf["dlogitsb"][:nz].copy_(buf["dlogits"][:nz])
         self._run(pl.bwd_enc)
-        if update:
+        if update and pl.skip is not None:
+            lib.adam_update(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                            self.pbf.data_ptr(), self.lr_t.data_ptr(), self.pa.size, self.b1, self.b2, self.eps,
+                            pl.skip.data_ptr(), s)
+        elif update:
             lib.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
                      self.step_i.data_ptr(), self.lr_t.data_ptr(), self.pa.size, float(lr), self.b1, self.b2,
                      self.eps, s)

@@ -94,6 +94,26 @@ def test_hip_training_is_bitwise_reproducible():
     assert torch.equal(arenas[0][0], arenas[1][0]) and torch.equal(arenas[0][1], arenas[1][1])
 
 
+def test_hip_fused_adam_matches_the_arena_pass(monkeypatch):
+    """The single-split Dense WGRADs apply Adam in their epilogue (GF_ADAM) and the arena pass skips those
+    parameters: after 3 steps every parameter, moment and bf16 copy is bitwise the unfused run's."""
+    from serann.riboae.hip_trainer import HipRiboTrainer
+    x, u = _batch(32, seed=4)
+    out = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SERANN_FUSE_ADAM", fuse)
+        m = _model(5).cuda().train()
+        tr = HipRiboTrainer(m, device="cuda")
+        for _ in range(3):
+            tr.step(x.cuda(), 0.3, 0.05, 3e-4, noise=u.cuda())
+        torch.cuda.synchronize()
+        pl = tr.plans[(32, True)]
+        out.append((tr.p.cpu(), tr.m.cpu(), tr.v.cpu(), tr.pbf.cpu(), pl.skip is not None))
+    assert out[0][4] and not out[1][4]                   # the fused run did fuse
+    for a, b in zip(out[0][:4], out[1][:4]):
+        assert torch.equal(a, b)
+
+
 def test_hip_loss_curve_matches_torch_path(tmp_path):
     """200 scheduled training steps (trainer.train) on the HIP kernels and on the torch path: the
     smoothed loss at the end agrees within 2 %, and the HIP run leaves a loadable checkpoint."""
