@@ -513,20 +513,28 @@ constexpr int POOL_ELEMS = 1024;
 // math is 32-bit (the tensors of one organism stay far below 2^31 elements).
 __device__ __forceinline__ int pool_vec(int C) { return (C & 7) == 0 ? 8 : 1; }
 
+// Unit -> (pixel, channel) -> (image, row, column) index math by fp64 reciprocals: n * (1 / d) rounded down is
+// n / d exactly for 0 <= n < 2^31 and 1 <= d < 2^19 (the product's error is below 2^-21, the offset 2^-20 lifts
+// exact quotients over it, and a true fractional part is at most 1 - 2^-19).  The integer divisions they replace
+// (~30 instructions each, five to seven per unit) made the element-unit (C % 8 != 0) passes issue-bound.
+__device__ __forceinline__ double pinv(int d) { return 1.0 / (double)d; }
+__device__ __forceinline__ int pdiv(int n, double inv) { return (int)fma((double)n, inv, 0x1p-20); }
+
 template <int V>
 __device__ __forceinline__ void pool_fwd_units(const PoolDesc& d, int u0, int u1) {
     const int C = (int)d.C, OW = (int)d.OW, OH = (int)d.OH, W = (int)d.W, H = (int)d.H;
     const int PH = (int)d.PH, PW = (int)d.PW, SH = (int)d.SH, SW = (int)d.SW;
     const int CV = C / V;
+    const double iCV = pinv(CV), iOHW = pinv(OH * OW), iOW = pinv(OW);
     const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(d.x);
     bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(d.y);
     uint8_t* __restrict__ idx = reinterpret_cast<uint8_t*>(d.idx);
     for (int u = u0 + (int)threadIdx.x; u < u1; u += blockDim.x) {
-        const int pix = u / CV;
+        const int pix = pdiv(u, iCV);
         const int c = (u - pix * CV) * V;
-        const int b = pix / (OH * OW);
+        const int b = pdiv(pix, iOHW);
         const int r = pix - b * (OH * OW);
-        const int oh = r / OW, ow = r - (r / OW) * OW;
+        const int oh = pdiv(r, iOW), ow = r - oh * OW;
         float best[V];
         uint8_t bi[V];
 #pragma unroll
@@ -563,20 +571,31 @@ __device__ __forceinline__ void pool_bwd_units(const PoolDesc& d, int u0, int u1
     const int C = (int)d.C, OW = (int)d.OW, OH = (int)d.OH, W = (int)d.W, H = (int)d.H;
     const int PH = (int)d.PH, PW = (int)d.PW, SH = (int)d.SH, SW = (int)d.SW;
     const int CV = C / V;
+    const double iCV = pinv(CV), iHW = pinv(H * W), iW = pinv(W), iSH = pinv(SH), iSW = pinv(SW);
+    // non-overlapping windows (strides = pool size, Keras' default): an input element lies in at most one window
+    const bool tiled = SH == PH && SW == PW;
     const bf16_t* __restrict__ dy = reinterpret_cast<const bf16_t*>(d.dy);
     bf16_t* __restrict__ dx = reinterpret_cast<bf16_t*>(d.dx);
     const uint8_t* __restrict__ idx = reinterpret_cast<const uint8_t*>(d.idx);
     for (int u = u0 + (int)threadIdx.x; u < u1; u += blockDim.x) {
-        const int pix = u / CV;
+        const int pix = pdiv(u, iCV);
         const int c = (u - pix * CV) * V;
-        const int b = pix / (H * W);
+        const int b = pdiv(pix, iHW);
         const int r = pix - b * (H * W);
-        const int ih = r / W, iw = r - (r / W) * W;
+        const int ih = pdiv(r, iW), iw = r - ih * W;
         float acc[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) acc[j] = 0.f;
-        const int oh_lo = max(0, (ih - PH + SH) / SH), oh_hi = min(OH - 1, ih / SH);
-        const int ow_lo = max(0, (iw - PW + SW) / SW), ow_hi = min(OW - 1, iw / SW);
+        int oh_lo, oh_hi, ow_lo, ow_hi;
+        if (tiled) {
+            oh_lo = oh_hi = pdiv(ih, iSH);
+            ow_lo = ow_hi = pdiv(iw, iSW);
+            if (oh_lo >= OH) oh_hi = -1;                  // past the last window: no window, zero gradient
+            if (ow_lo >= OW) ow_hi = -1;
+        } else {
+            oh_lo = max(0, pdiv(max(ih - PH + SH, 0), iSH)); oh_hi = min(OH - 1, pdiv(ih, iSH));
+            ow_lo = max(0, pdiv(max(iw - PW + SW, 0), iSW)); ow_hi = min(OW - 1, pdiv(iw, iSW));
+        }
         for (int oh = oh_lo; oh <= oh_hi; ++oh) {
             const int i = ih - oh * SH;
             if (i < 0 || i >= PH) continue;

@@ -331,10 +331,10 @@ def test_bn_train_infer_backward(RC):
 
 @pytest.mark.parametrize("C", [5, 16])
 @pytest.mark.parametrize("p", [(2, 2, 2, 2), (3, 3, 3, 3), (3, 3, 2, 2), (2, 3, 1, 2)])
-def test_maxpool_fwd_bwd(p, C):
+def test_maxpool_fwd_bwd(p, C, shape=(3, 13, 11)):
     """C=5: element units; C=16: 8-channel vector units (aux.hip pool_vec)."""
     PH, PW, SH, SW = p
-    B, Hh, Ww = 3, 13, 11
+    B, Hh, Ww = shape
     OH, OW = (Hh - PH) // SH + 1, (Ww - PW) // SW + 1
     x = H.padded(torch.randn(B, Hh, Ww, C, device=DEV).bfloat16())
     y = H.padded(torch.zeros(B, OH, OW, C, dtype=torch.bfloat16, device=DEV))
@@ -355,6 +355,14 @@ def test_maxpool_fwd_bwd(p, C):
     assert torch.equal(y.float(), ref.detach().permute(0, 2, 3, 1))
     ref.backward(dy.float().permute(0, 3, 1, 2))
     assert _rel(dx.float(), xf.grad.permute(0, 2, 3, 1)) < 6e-3
+
+
+@pytest.mark.parametrize("C", [37, 8])
+@pytest.mark.parametrize("p", [(2, 2, 2, 2), (3, 3, 2, 2)])
+def test_maxpool_large_unit_indices(p, C):
+    """~2^24 element units (a batch-750 conv output with an odd filter count): the fp64-reciprocal index math of
+    aux.hip's pool kernels stays exact past float32's integer range."""
+    test_maxpool_fwd_bwd(p, C, shape=(750, 27, 25))
 
 
 def test_loss_kernel_matches_keras_losses():
