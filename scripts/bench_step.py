@@ -70,7 +70,8 @@ def main():
         wall = time.perf_counter() - t0
         print(f"streams={ns} organisms={len(irs)} steps={fit.steps} init_s={init_s:.3f} plan_s={eng.timings['plan_s']:.3f} "
               f"loop_s={fit.learning_time:.3f} ms/step={1e3 * fit.learning_time / fit.steps:.2f} "
-              f"launches/step={eng.timings['launches_per_step']} fit_wall={wall:.2f}", flush=True)
+              f"launches/step={eng.timings['launches_per_step']} fit_wall={wall:.2f} "
+              f"replay_ms/step={eng.timings.get('replay_ms_per_step', float('nan')):.2f}", flush=True)
         eng.close()
         del eng
 
