@@ -2440,9 +2440,6 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         // and stores them to NbnDesc::part, slot m tile -- plain stores, one writer per (slot, column).  nbn
         // phase 6 adds the slots in a fixed order and forms dgamma, dbeta, dW, db.
         constexpr int NSUM = 8;
-#ifndef NBNSUM_AB_SKIP
-#define NBNSUM_AB_SKIP 0          // measurement builds only (-DNBNSUM_AB_SKIP=1): the column sums are skipped
-#endif
         const NbnDesc& nd = *reinterpret_cast<const NbnDesc*>(d.ext);
         const int Fb = (int)nd.F, ldxr = (int)nd.ldx, NPc = (int)nd.np, nact = (int)nd.act;
         const bf16_t* __restrict__ Xr = reinterpret_cast<const bf16_t*>(nd.x);
@@ -2536,7 +2533,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             float sm[NSUM];
 #pragma unroll
             for (int q = 0; q < NSUM; ++q) sm[q] = 0.f;
-            if (n < N && !NBNSUM_AB_SKIP) {
+            if (n < N) {
                 const int p = n / Fb, f = n - p * Fb;
                 const float w = bf2f(Wn[f]), bv = nb ? nb[f] : 0.f, mu = nmean[f], is = nis[f];
                 const float* xc = xs + (p - p0) * SLT + sg * 16;
