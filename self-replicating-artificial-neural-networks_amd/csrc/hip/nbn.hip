@@ -305,12 +305,14 @@ __global__ __launch_bounds__(1024) void nbn_fin_kernel(const NbnDesc* __restrict
     if (t < nch) {
         const int f = f0 + t;
         double S[NBN_NSUM];
+        // (pq outermost and not unrolled: the fully unrolled 16 x 8 double loads were hoisted into registers and
+        // spilled 548 B of scratch per thread for the whole 1024-thread block)
 #pragma unroll
-        for (int k = 0; k < NBN_NSUM; ++k) {
-            S[k] = 0.0;
+        for (int k = 0; k < NBN_NSUM; ++k) S[k] = 0.0;
+#pragma unroll 1
+        for (int pq = 0; pq < NBN_FIN_PARTS; ++pq)
 #pragma unroll
-            for (int pq = 0; pq < NBN_FIN_PARTS; ++pq) S[k] += tot[pq][t * NBN_NSUM + k];   // fixed order
-        }
+            for (int k = 0; k < NBN_NSUM; ++k) S[k] += tot[pq][t * NBN_NSUM + k];   // fixed order per sum
         const double Rf = (double)d.R;
         const double is = reinterpret_cast<const float*>(d.invstd)[f];
         const double gg = ((d.flags & 1) ? (double)reinterpret_cast<const float*>(d.gamma)[f] : 1.0) * is;
