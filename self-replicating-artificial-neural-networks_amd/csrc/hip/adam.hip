@@ -17,12 +17,14 @@ __global__ void adam_scalars_kernel(int* step, float* lr_t, float lr, float b1, 
 }
 
 // skip (optional): one byte per 4-parameter group, bit j set = parameter 4i + j was already updated by its
-// WGRAD epilogue (GF_ADAM) this step; fully skipped groups are not even read.
+// WGRAD epilogue (GF_ADAM) this step; fully skipped groups are not even read.  MM: moment storage (common.h).
+template <int MM>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long long* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   void* __restrict__ m, void* __restrict__ v,
                                                    bf16_t* __restrict__ pbf, const float* __restrict__ lr_t_ptr,
                                                    int64_t n, float b1, float b2, float eps,
-                                                   const uint8_t* __restrict__ skip) {
+                                                   const uint8_t* __restrict__ skip, const int64_t* __restrict__ org_off,
+                                                   int* __restrict__ diverged, int norg) {
     const float lr_t = *lr_t_ptr;
     const int64_t n4 = n >> 2;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -33,8 +35,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long l
         const longlong2 g01 = reinterpret_cast<longlong2*>(g)[2 * i];
         const longlong2 g23 = reinterpret_cast<longlong2*>(g)[2 * i + 1];
         float4 gv = make_float4(fx_f(g01.x), fx_f(g01.y), fx_f(g23.x), fx_f(g23.y));
-        float4 mv = reinterpret_cast<float4*>(m)[i];
-        float4 vv = reinterpret_cast<float4*>(v)[i];
+        if (org_off && fmaxf(fmaxf(fabsf(gv.x), fabsf(gv.y)), fmaxf(fabsf(gv.z), fabsf(gv.w))) > FX_DIVERGE)
+            flag_diverged(org_off, diverged, norg, 4 * i);
+        float4 mv = m_ld4<MM>(m, 4 * i);
+        float4 vv = v_ld4<MM>(v, 4 * i);
         float* pp = &pv.x; float* gg = &gv.x; float* mm = &mv.x; float* vvv = &vv.x;
         ushort4 ob = reinterpret_cast<ushort4*>(pbf)[i];
         uint16_t* o = &ob.x;
@@ -45,8 +49,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long l
                 o[k] = f2bf(pp[k]);
             }
             reinterpret_cast<float4*>(p)[i] = pv;
-            reinterpret_cast<float4*>(m)[i] = mv;
-            reinterpret_cast<float4*>(v)[i] = vv;
+            m_st4<MM>(m, 4 * i, mv);
+            v_st4<MM>(v, 4 * i, vv);
             reinterpret_cast<longlong2*>(g)[2 * i] = make_longlong2(0, 0);
             reinterpret_cast<longlong2*>(g)[2 * i + 1] = make_longlong2(0, 0);
             reinterpret_cast<ushort4*>(pbf)[i] = ob;
@@ -57,16 +61,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, long l
                 if (sk & (1u << k)) continue;
                 const int64_t e = 4 * i + k;
                 adam_elem(pp[k], mm[k], vvv[k], gg[k], lr_t, b1, b2, eps);
-                p[e] = pp[k]; m[e] = mm[k]; v[e] = vvv[k]; g[e] = 0; pbf[e] = f2bf(pp[k]);
+                p[e] = pp[k]; m_st<MM>(m, e, mm[k]); v_st<MM>(v, e, vvv[k]); g[e] = 0; pbf[e] = f2bf(pp[k]);
             }
         }
     }
     // tail
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (skip && ((skip[i >> 2] >> (i & 3)) & 1u)) continue;
-        float pp = p[i], mm = m[i], vv = v[i];
+        float pp = p[i], mm = m_ld<MM>(m, i), vv = v_ld<MM>(v, i);
+        if (org_off && fabsf(fx_f(g[i])) > FX_DIVERGE) flag_diverged(org_off, diverged, norg, i);
         adam_elem(pp, mm, vv, fx_f(g[i]), lr_t, b1, b2, eps);
-        m[i] = mm; v[i] = vv; p[i] = pp; g[i] = 0; pbf[i] = f2bf(pp);
+        m_st<MM>(m, i, mm); v_st<MM>(v, i, vv); p[i] = pp; g[i] = 0; pbf[i] = f2bf(pp);
     }
 }
 
@@ -81,21 +86,25 @@ void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float
 }
 
 void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
-                        float b1, float b2, float eps, uint64_t skip, uint64_t stream) {
+                        float b1, float b2, float eps, uint64_t skip, uint64_t stream, int mode, uint64_t org_off,
+                        uint64_t diverged, int64_t norg) {
     if (n <= 0) return;
+    if (mode != MOM_F32 && mode != MOM_16) throw std::runtime_error("adam_update: unknown moment mode");
     int64_t blocks = ((n >> 2) + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), as_ptr<float>(p),
-                       as_ptr<long long>(g), as_ptr<float>(m), as_ptr<float>(v), as_ptr<bf16_t>(pbf),
-                       as_ptr<const float>(lr_t), n, b1, b2, eps, as_ptr<const uint8_t>(skip));
+    auto kern = mode == MOM_16 ? adam_kernel<MOM_16> : adam_kernel<MOM_F32>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), as_ptr<float>(p),
+                       as_ptr<long long>(g), as_ptr<void>(m), as_ptr<void>(v), as_ptr<bf16_t>(pbf),
+                       as_ptr<const float>(lr_t), n, b1, b2, eps, as_ptr<const uint8_t>(skip),
+                       as_ptr<const int64_t>(norg > 0 ? org_off : 0), as_ptr<int>(diverged), (int)norg);
     SERANN_CHECK(hipGetLastError());
 }
 
 void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
-                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream) {
+                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream, int mode) {
     launch_adam_scalars(step, lr_t, lr, b1, b2, stream);
-    launch_adam_update(p, g, m, v, pbf, lr_t, n, b1, b2, eps, 0, stream);
+    launch_adam_update(p, g, m, v, pbf, lr_t, n, b1, b2, eps, 0, stream, mode, 0, 0, 0);
 }
 
 void launch_f32_to_bf16(uint64_t x, uint64_t y, int64_t n, uint64_t stream) {

@@ -961,11 +961,19 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
         // sole writer of this parameter: the optimizer step here (as the GF_ADAM WGRAD epilogue)
         const int64_t pe = (out - reinterpret_cast<const long long*>(ac->g)) + e;
         float* P = reinterpret_cast<float*>(ac->p);
-        float* Mo = reinterpret_cast<float*>(ac->m);
-        float* Vo = reinterpret_cast<float*>(ac->v);
-        float p_ = P[pe], m_ = Mo[pe], v_ = Vo[pe];
+        void* Mo = reinterpret_cast<void*>(ac->m);
+        void* Vo = reinterpret_cast<void*>(ac->v);
+        const bool m16 = ac->mode == MOM_16;
+        if (ac->org_off && fabsf(fx_f(q)) > FX_DIVERGE)
+            flag_diverged(reinterpret_cast<const int64_t*>(ac->org_off), reinterpret_cast<int*>(ac->diverged),
+                          (int)ac->norg, pe);
+        float p_ = P[pe];
+        float m_ = m16 ? m_ld<MOM_16>(Mo, pe) : m_ld<MOM_F32>(Mo, pe);
+        float v_ = m16 ? v_ld<MOM_16>(Vo, pe) : v_ld<MOM_F32>(Vo, pe);
         adam_elem(p_, m_, v_, fx_f(q), *reinterpret_cast<const float*>(ac->lr_t), ac->b1, ac->b2, ac->eps);
-        P[pe] = p_; Mo[pe] = m_; Vo[pe] = v_;
+        P[pe] = p_;
+        if (m16) { m_st<MOM_16>(Mo, pe, m_); v_st<MOM_16>(Vo, pe, v_); }
+        else { m_st<MOM_F32>(Mo, pe, m_); v_st<MOM_F32>(Vo, pe, v_); }
         reinterpret_cast<bf16_t*>(ac->pbf)[pe] = f2bf(p_);
     }
 }

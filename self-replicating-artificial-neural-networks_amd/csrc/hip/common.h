@@ -119,6 +119,25 @@ __device__ __forceinline__ double fxw_sum_d(const long long* ws, int C, int idx)
     return (double)hi + (double)lo * (1.0 / 4294967296.0);
 }
 
+// Divergence detection (the reference's fp16 semantics).  The Q40 arena wraps silently when a gradient sum leaves
+// +-2^23; a wrapped sum lands uniformly in [-2^23, 2^23), so it still exceeds fp16's largest finite value 65504 with
+// probability 0.99 per element -- and an exploding organism has many such elements.  Every Adam site (the arena pass
+// and the fused WGRAD / finalize epilogues) therefore flags the organism owning a gradient element with
+// |g| > FX_DIVERGE: in the reference's float16 graph that gradient is inf, the weights become NaN and so do the
+// organism's metrics (experiment_worker.py:36-37); the engine reports the flagged organisms' metrics as NaN
+// (fertility 0, as for an invalid organism).  org_off: int64 [norg + 1] first arena element of each organism
+// (ascending; the parameter arena is laid out organism by organism); diverged: int32 [norg].
+constexpr float FX_DIVERGE = 65504.f;
+__device__ __noinline__ void flag_diverged(const int64_t* __restrict__ org_off, int* __restrict__ diverged, int norg,
+                                           int64_t e) {
+    int lo = 0, hi = norg - 1;                       // the last organism whose first element is <= e
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (org_off[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    diverged[lo] = 1;
+}
+
 // Keras / TF ResourceApplyAdam on one element (experiment_worker.py:80): shared by the arena-wide Adam pass
 // and the WGRAD epilogues that apply the step to their own tile (GF_ADAM), so both give the same bits.
 // Every operation is spelled out (explicit fma, IEEE sqrt and division, no contraction) so the two call
@@ -130,6 +149,82 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
     v = __fmaf_rn(b2, v, ((1.f - b2) * g) * g);
     const float den = __fsqrt_rn(v) + eps;
     p = p - __fdiv_rn(lr_t * m, den);
+}
+
+// Adam moment storage (AdamCtx::mode, adam_kernel<MM>).  MOM_F32: fp32 m and v.  MOM_16: both moments in 16 bits,
+// as the reference keeps them (fp16 floatx: experiment_worker.py:36-37, optimizer :80), master weights fp32:
+//  * m: bf16 (RNE).  b1 = 0.9 moves m by 10 % of (g - m) per step, far above bf16's half ulp (2^-9), so the EMA
+//    tracks; the stored value carries 0.4 % relative error into the update.
+//  * v: "log16", q = rint(1024 log2 v) as int16 (q = -32768: v = 0; v < 2^-32 flushes to 0, v > 2^32 saturates).
+//    An EMA with b2 = 0.999 moves v by 0.1 % of (g^2 - v) per step: in bf16 (half ulp 0.2 %) that increment rounds
+//    away unless g^2 > 3 v, so v would freeze.  log16's adjacent values differ by 2^(1/1024) (half ulp 0.034 %, fp16's
+//    relative precision) over 2^-32 .. 2^32 -- fp16 itself flushes v below 6e-8 (|g| < 2.4e-4) and overflows at
+//    65504.  sqrt(v) = 2^(q / 2048) is what the update reads.
+// The arithmetic is adam_elem's in fp32 either way; the moments are rounded once when stored.  18 B per parameter
+// and step instead of 26 in the fused WGRAD epilogues (p 4+4, m 2+2, v 2+2, bf16 shadow 2).
+constexpr int MOM_F32 = 0, MOM_16 = 1;
+__device__ __forceinline__ float log16_f(int16_t q) {
+    return q == (int16_t)-32768 ? 0.f : __builtin_amdgcn_exp2f((float)q * (1.f / 1024.f));
+}
+__device__ __forceinline__ int16_t log16_q(float v) {
+    if (!(v >= 2.3283064e-10f)) return (int16_t)-32768;          // 0, < 2^-32 (and NaN, never produced)
+    const float l = fminf(__builtin_amdgcn_logf(v) * 1024.f, 32767.f);
+    return (int16_t)__float2int_rn(l);
+}
+template <int MM>
+__device__ __forceinline__ float m_ld(const void* b, int64_t e) {
+    if constexpr (MM == MOM_16) return bf2f(reinterpret_cast<const bf16_t*>(b)[e]);
+    else return reinterpret_cast<const float*>(b)[e];
+}
+template <int MM>
+__device__ __forceinline__ void m_st(void* b, int64_t e, float x) {
+    if constexpr (MM == MOM_16) reinterpret_cast<bf16_t*>(b)[e] = f2bf(x);
+    else reinterpret_cast<float*>(b)[e] = x;
+}
+template <int MM>
+__device__ __forceinline__ float v_ld(const void* b, int64_t e) {
+    if constexpr (MM == MOM_16) return log16_f(reinterpret_cast<const int16_t*>(b)[e]);
+    else return reinterpret_cast<const float*>(b)[e];
+}
+template <int MM>
+__device__ __forceinline__ void v_st(void* b, int64_t e, float x) {
+    if constexpr (MM == MOM_16) reinterpret_cast<int16_t*>(b)[e] = log16_q(x);
+    else reinterpret_cast<float*>(b)[e] = x;
+}
+// four consecutive moments, e % 4 == 0 (16-B fp32 / 8-B 16-bit vectors)
+template <int MM>
+__device__ __forceinline__ float4 m_ld4(const void* b, int64_t e) {
+    if constexpr (MM == MOM_16) {
+        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(b) + e);
+        return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    } else {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(b) + e);
+    }
+}
+template <int MM>
+__device__ __forceinline__ void m_st4(void* b, int64_t e, float4 x) {
+    if constexpr (MM == MOM_16)
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(b) + e) = make_uint2(f2bf2(x.x, x.y), f2bf2(x.z, x.w));
+    else
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(b) + e) = x;
+}
+template <int MM>
+__device__ __forceinline__ float4 v_ld4(const void* b, int64_t e) {
+    if constexpr (MM == MOM_16) {
+        const short4 q = *reinterpret_cast<const short4*>(reinterpret_cast<const int16_t*>(b) + e);
+        return make_float4(log16_f(q.x), log16_f(q.y), log16_f(q.z), log16_f(q.w));
+    } else {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(b) + e);
+    }
+}
+template <int MM>
+__device__ __forceinline__ void v_st4(void* b, int64_t e, float4 x) {
+    if constexpr (MM == MOM_16)
+        *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(b) + e) =
+            make_short4(log16_q(x.x), log16_q(x.y), log16_q(x.z), log16_q(x.w));
+    else
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(b) + e) = x;
 }
 
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }

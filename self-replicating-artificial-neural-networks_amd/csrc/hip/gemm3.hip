@@ -614,6 +614,153 @@ __device__ __forceinline__ void wait_vmcnt() {       // s_waitcnt vmcnt(N) only 
 // Flush of a Dense / 1x1 WGRAD tile (g3_wgrad_kernel, g3_dwgrad_kernel): a lane holds rows frow0 + i * 16 + 4 * (lane / 16)
 // + r and columns kcol0 + j * 16 + lane % 16 of its TF x TK accumulator tiles.  Fused Adam (sole writer), plain
 // Q40 store (sole writer) or fixed-point atomics (m-split).
+// Fused-Adam flush of a sole-writer WGRAD tile (GF_WSTORE | GF_ADAM): the optimizer step applied to the tile, the
+// gradient quantised exactly as the Q40 arena would hold it (the arena-wide Adam pass skips these parameters).
+// MM: storage of the moment arenas (common.h MOM_*).
+template <int MM, int TF, int TK>
+__device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g, f32x4_t (&acc)[TF][TK], int frow0,
+                                                 int kcol0, int lane, float* stage, int wave) {
+    const int c16 = lane & 15, rq = (lane >> 4) * 4;
+    const long long* out = reinterpret_cast<const long long*>(d.out);
+    const int ldo = d.ldo ? (int)d.ldo : g.N;
+    const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
+    const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
+    float* __restrict__ P = reinterpret_cast<float*>(ac.p);
+    void* __restrict__ Mo = reinterpret_cast<void*>(ac.m);
+    void* __restrict__ Vo = reinterpret_cast<void*>(ac.v);
+    bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
+    const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+    auto chk = [&](float gq, int64_t e) {            // common.h flag_diverged
+        if (ac.org_off && fabsf(gq) > FX_DIVERGE)
+            flag_diverged(reinterpret_cast<const int64_t*>(ac.org_off), reinterpret_cast<int*>(ac.diverged), (int)ac.norg, e);
+    };
+    if (stage != nullptr) {
+        // Row-major through LDS (stage: 2 x TR x LD floats; the k loop's tiles are dead): a lane of the
+        // accumulator layout holds 4 rows x 1 column of each 16 x 16 tile, so updating in place read and wrote
+        // p / m / v / pbf as 64-B quarter rows, one element per lane per instruction.  Staged, a lane takes 4
+        // consecutive columns of one row: 16-B accesses, whole 256-B row segments per 16 lanes, a quarter of the
+        // memory instructions.  Two rounds of two waves (the LDS holds two wave tiles).
+        // Every wave issues the p / m / v loads of all its NIT row passes first, before the two LDS rounds: one
+        // memory round trip per wave instead of NIT serial ones (a pass's loads could not move above the previous
+        // pass's stores through possibly aliasing pointers), and the second round's loads fly during the first.
+        constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG, NIT = TR / RPI;
+        using MT = typename std::conditional<MM == MOM_16, uint2, float4>::type;
+        const int64_t t0 = e0 + (int64_t)frow0 * ldo + kcol0;
+        const bool vec = (t0 & 3) == 0 && (ldo & 3) == 0;      // float4-aligned rows
+        const int cg = lane % CG, rr = lane / CG;
+        const int col = kcol0 + cg * 4;
+        float4 pr[NIT];
+        MT mr[NIT], vr[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int row = frow0 + it * RPI + rr;
+            if (vec && row < g.M && col + 4 <= g.N) {
+                const int64_t e = e0 + (int64_t)row * ldo + col;
+                pr[it] = *reinterpret_cast<const float4*>(&P[e]);
+                if constexpr (MM == MOM_16) {
+                    mr[it] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(Mo) + e);
+                    vr[it] = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(Vo) + e);
+                } else {
+                    mr[it] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Mo) + e);
+                    vr[it] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Vo) + e);
+                }
+            }
+        }
+        for (int half = 0; half < 2; ++half) {
+            __syncthreads();
+            if ((wave >> 1) == half) {
+                float* st = stage + (wave & 1) * TR * LD;
+#pragma unroll
+                for (int i = 0; i < TF; ++i)
+#pragma unroll
+                    for (int j = 0; j < TK; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) st[(i * 16 + rq + r) * LD + j * 16 + c16] = acc[i][j][r];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int it = 0; it < NIT; ++it) {
+                    const int row = frow0 + it * RPI + rr;
+                    if (row >= g.M || col >= g.N) continue;
+                    const float4 gv = *reinterpret_cast<const float4*>(&st[(it * RPI + rr) * LD + cg * 4]);
+                    const int64_t e = e0 + (int64_t)row * ldo + col;
+                    chk(fmaxf(fmaxf(fabsf(gv.x), fabsf(gv.y)), fmaxf(fabsf(gv.z), fabsf(gv.w))), e);
+                    if (vec && col + 4 <= g.N) {
+                        float4 p4 = pr[it], m4, v4;
+                        if constexpr (MM == MOM_16) {
+                            const uint2 u = mr[it];
+                            m4 = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                             __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+                            const uint2 w = vr[it];
+                            v4 = make_float4(log16_f((int16_t)(w.x & 0xffffu)), log16_f((int16_t)(w.x >> 16)),
+                                             log16_f((int16_t)(w.y & 0xffffu)), log16_f((int16_t)(w.y >> 16)));
+                        } else {
+                            m4 = mr[it];
+                            v4 = vr[it];
+                        }
+                        adam_elem(p4.x, m4.x, v4.x, fx_f(fx_q(gv.x)), lr_t, ac.b1, ac.b2, ac.eps);
+                        adam_elem(p4.y, m4.y, v4.y, fx_f(fx_q(gv.y)), lr_t, ac.b1, ac.b2, ac.eps);
+                        adam_elem(p4.z, m4.z, v4.z, fx_f(fx_q(gv.z)), lr_t, ac.b1, ac.b2, ac.eps);
+                        adam_elem(p4.w, m4.w, v4.w, fx_f(fx_q(gv.w)), lr_t, ac.b1, ac.b2, ac.eps);
+                        *reinterpret_cast<float4*>(&P[e]) = p4;
+                        m_st4<MM>(Mo, e, m4);
+                        v_st4<MM>(Vo, e, v4);
+                        *reinterpret_cast<uint2*>(&Pb[e]) = make_uint2(f2bf2(p4.x, p4.y), f2bf2(p4.z, p4.w));
+                    } else {
+                        const float gq[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            if (col + q >= g.N) break;
+                            float p_ = P[e + q], m_ = m_ld<MM>(Mo, e + q), v_ = v_ld<MM>(Vo, e + q);
+                            adam_elem(p_, m_, v_, fx_f(fx_q(gq[q])), lr_t, ac.b1, ac.b2, ac.eps);
+                            P[e + q] = p_; m_st<MM>(Mo, e + q, m_); v_st<MM>(Vo, e + q, v_); Pb[e + q] = f2bf(p_);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
+    // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
+    // and stored -- element by element, each load waited behind the previous element's stores (the
+    // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
+    // round trips per lane in the epilogue, now TF (one batch of TK x 4 x 3 loads in flight each)
+#pragma unroll
+    for (int i = 0; i < TF; ++i) {
+        float pv[TK][4], mv[TK][4], vv[TK][4];
+#pragma unroll
+        for (int j = 0; j < TK; ++j) {
+            const int col = kcol0 + j * 16 + c16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = frow0 + i * 16 + rq + r;
+                if (col < g.N && row < g.M) {
+                    const int64_t e = e0 + (int64_t)row * ldo + col;
+                    pv[j][r] = P[e];
+                    mv[j][r] = m_ld<MM>(Mo, e);
+                    vv[j][r] = v_ld<MM>(Vo, e);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TK; ++j) {
+            const int col = kcol0 + j * 16 + c16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = frow0 + i * 16 + rq + r;
+                if (col < g.N && row < g.M) {
+                    const int64_t e = e0 + (int64_t)row * ldo + col;
+                    float p_ = pv[j][r], m_ = mv[j][r], v_ = vv[j][r];
+                    chk(acc[i][j][r], e);
+                    adam_elem(p_, m_, v_, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
+                    P[e] = p_; m_st<MM>(Mo, e, m_); v_st<MM>(Vo, e, v_); Pb[e] = f2bf(p_);
+                }
+            }
+        }
+    }
+}
+
 template <int TF, int TK>
 __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x4_t (&acc)[TF][TK], int frow0,
                                             int kcol0, int lane, float* stage = nullptr, int wave = 0) {
@@ -621,106 +768,10 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
     long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
     if ((g.flags & (GF_WSTORE | GF_ADAM)) == (GF_WSTORE | GF_ADAM)) {
-        // sole writer of this tile: apply the optimizer step here (the gradient quantised exactly as the
-        // Q40 arena would hold it) -- the arena-wide Adam pass skips these parameters
-        const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
-        const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
-        float* __restrict__ P = reinterpret_cast<float*>(ac.p);
-        float* __restrict__ Mo = reinterpret_cast<float*>(ac.m);
-        float* __restrict__ Vo = reinterpret_cast<float*>(ac.v);
-        bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
-        const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
-        if (stage != nullptr) {
-            // Row-major through LDS (stage: 2 x TR x LD floats; the k loop's tiles are dead): a lane of the
-            // accumulator layout holds 4 rows x 1 column of each 16 x 16 tile, so updating in place read and wrote
-            // p / m / v / pbf as 64-B quarter rows, one element per lane per instruction.  Staged, a lane takes 4
-            // consecutive columns of one row: 16-B accesses, whole 256-B row segments per 16 lanes, a quarter of the
-            // memory instructions.  Two rounds of two waves (the LDS holds two wave tiles).
-            constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG;
-            const int64_t t0 = e0 + (int64_t)frow0 * ldo + kcol0;
-            const bool vec = (t0 & 3) == 0 && (ldo & 3) == 0;      // float4-aligned rows
-            const int cg = lane % CG, rr = lane / CG;
-            for (int half = 0; half < 2; ++half) {
-                __syncthreads();
-                if ((wave >> 1) == half) {
-                    float* st = stage + (wave & 1) * TR * LD;
-#pragma unroll
-                    for (int i = 0; i < TF; ++i)
-#pragma unroll
-                        for (int j = 0; j < TK; ++j)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) st[(i * 16 + rq + r) * LD + j * 16 + c16] = acc[i][j][r];
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    for (int r0 = 0; r0 < TR; r0 += RPI) {
-                        const int row = frow0 + r0 + rr, col = kcol0 + cg * 4;
-                        if (row >= g.M || col >= g.N) continue;
-                        const float4 gv = *reinterpret_cast<const float4*>(&st[(r0 + rr) * LD + cg * 4]);
-                        const int64_t e = e0 + (int64_t)row * ldo + col;
-                        if (vec && col + 4 <= g.N) {
-                            float4 p4 = *reinterpret_cast<const float4*>(&P[e]);
-                            float4 m4 = *reinterpret_cast<const float4*>(&Mo[e]);
-                            float4 v4 = *reinterpret_cast<const float4*>(&Vo[e]);
-                            adam_elem(p4.x, m4.x, v4.x, fx_f(fx_q(gv.x)), lr_t, ac.b1, ac.b2, ac.eps);
-                            adam_elem(p4.y, m4.y, v4.y, fx_f(fx_q(gv.y)), lr_t, ac.b1, ac.b2, ac.eps);
-                            adam_elem(p4.z, m4.z, v4.z, fx_f(fx_q(gv.z)), lr_t, ac.b1, ac.b2, ac.eps);
-                            adam_elem(p4.w, m4.w, v4.w, fx_f(fx_q(gv.w)), lr_t, ac.b1, ac.b2, ac.eps);
-                            *reinterpret_cast<float4*>(&P[e]) = p4;
-                            *reinterpret_cast<float4*>(&Mo[e]) = m4;
-                            *reinterpret_cast<float4*>(&Vo[e]) = v4;
-                            *reinterpret_cast<uint2*>(&Pb[e]) = make_uint2(f2bf2(p4.x, p4.y), f2bf2(p4.z, p4.w));
-                        } else {
-                            const float gq[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                if (col + q >= g.N) break;
-                                float p_ = P[e + q], m_ = Mo[e + q], v_ = Vo[e + q];
-                                adam_elem(p_, m_, v_, fx_f(fx_q(gq[q])), lr_t, ac.b1, ac.b2, ac.eps);
-                                P[e + q] = p_; Mo[e + q] = m_; Vo[e + q] = v_; Pb[e + q] = f2bf(p_);
-                            }
-                        }
-                    }
-                }
-            }
-            return;
-        }
-        // per 16-row f tile i: every (p, m, v) of the lane's TK x 4 elements is loaded first, then updated
-        // and stored -- element by element, each load waited behind the previous element's stores (the
-        // compiler cannot move loads over stores through possibly aliasing pointers): up to 32 serial memory
-        // round trips per lane in the epilogue, now TF (one batch of TK x 4 x 3 loads in flight each)
-#pragma unroll
-        for (int i = 0; i < TF; ++i) {
-            float pv[TK][4], mv[TK][4], vv[TK][4];
-#pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int col = kcol0 + j * 16 + c16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = frow0 + i * 16 + rq + r;
-                    if (col < g.N && row < g.M) {
-                        const int64_t e = e0 + (int64_t)row * ldo + col;
-                        pv[j][r] = P[e];
-                        mv[j][r] = Mo[e];
-                        vv[j][r] = Vo[e];
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int col = kcol0 + j * 16 + c16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = frow0 + i * 16 + rq + r;
-                    if (col < g.N && row < g.M) {
-                        const int64_t e = e0 + (int64_t)row * ldo + col;
-                        float p_ = pv[j][r], m_ = mv[j][r], v_ = vv[j][r];
-                        adam_elem(p_, m_, v_, fx_f(fx_q(acc[i][j][r])), lr_t, ac.b1, ac.b2, ac.eps);
-                        P[e] = p_; Mo[e] = m_; Vo[e] = v_; Pb[e] = f2bf(p_);
-                    }
-                }
-            }
-        }
+        if (reinterpret_cast<const AdamCtx*>(d.adam)->mode == MOM_16)
+            wgrad_adam_flush<MOM_16, TF, TK>(d, g, acc, frow0, kcol0, lane, stage, wave);
+        else
+            wgrad_adam_flush<MOM_F32, TF, TK>(d, g, acc, frow0, kcol0, lane, stage, wave);
         return;
     }
     if (stage != nullptr && (g.flags & GF_WSTORE)) {

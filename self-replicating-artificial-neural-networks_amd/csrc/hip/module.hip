@@ -38,14 +38,18 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("gemm3", &launch_gemm3, py::arg("mode"), py::arg("variant"), py::arg("descs"), py::arg("tiles"),
           py::arg("ntiles"), py::arg("stream"));
     m.def("transpose_weights", &launch_transpose_weights);
-    m.def("adam", &launch_adam);
+    m.def("adam", &launch_adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pbf"), py::arg("step"),
+          py::arg("lr_t"), py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("stream"),
+          py::arg("mode") = 0);
     m.def("f32_to_bf16", &launch_f32_to_bf16);
     m.def("gather_batch", &launch_gather_batch);
     m.def("counter_add", &launch_counter_add);
     m.def("bn", &launch_bn);
     m.def("nbn", &launch_nbn);
     m.def("adam_scalars", &launch_adam_scalars);
-    m.def("adam_update", &launch_adam_update);
+    m.def("adam_update", &launch_adam_update, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("pbf"),
+          py::arg("lr_t"), py::arg("n"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("skip"), py::arg("stream"),
+          py::arg("mode") = 0, py::arg("org_off") = 0, py::arg("diverged") = 0, py::arg("norg") = 0);
     m.def("pool", &launch_pool);
     m.def("convpool", &launch_convpool);
     m.def("gchain", &launch_gchain);

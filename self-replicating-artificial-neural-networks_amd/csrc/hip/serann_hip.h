@@ -24,8 +24,10 @@ struct GemmDesc {
 // The parameter / gradient / moment arenas of a population engine (same layout, element e of each is the
 // same parameter) and the device Adam scalars, for WGRAD epilogues that apply the optimizer step (GF_ADAM).
 struct AdamCtx {
-    int64_t p, m, v, pbf, g, lr_t;   // fp32, fp32, fp32, bf16, Q40 int64 arenas; device lr_t (float)
-    float b1, b2, eps, pad;
+    int64_t p, m, v, pbf, g, lr_t;   // fp32, m / v (fp32, or bf16 / log16: mode), bf16, Q40 int64 arenas; device lr_t (float)
+    int64_t org_off, diverged, norg; // divergence flags (common.h flag_diverged; org_off = 0: none)
+    float b1, b2, eps;
+    int32_t mode;                    // common.h MOM_F32 / MOM_16: storage of the m and v arenas
 };
 enum GemmFlags : int64_t {
     GF_VEC_A = 1,         // A operand chunks are contiguous 8-element vectors
@@ -56,7 +58,7 @@ void launch_transpose_weights(uint64_t descs, uint64_t tiles, int64_t ntiles, ui
 
 // ---- optimizer --------------------------------------------------------------------------------
 void launch_adam(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t step, uint64_t lr_t,
-                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream);
+                 int64_t n, float lr, float b1, float b2, float eps, uint64_t stream, int mode);
 void launch_f32_to_bf16(uint64_t x, uint64_t y, int64_t n, uint64_t stream);
 
 // ---- auxiliary grouped kernels (aux.hip) ------------------------------------------------------
@@ -165,7 +167,8 @@ constexpr int NBN_NSUM = 8;
 // sizes the ranges (hip_ops.nbn_tiles)
 void launch_adam_scalars(uint64_t step, uint64_t lr_t, float lr, float b1, float b2, uint64_t stream);
 void launch_adam_update(uint64_t p, uint64_t g, uint64_t m, uint64_t v, uint64_t pbf, uint64_t lr_t, int64_t n,
-                        float b1, float b2, float eps, uint64_t skip, uint64_t stream);
+                        float b1, float b2, float eps, uint64_t skip, uint64_t stream, int mode, uint64_t org_off,
+                        uint64_t diverged, int64_t norg);
 void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_rep_bits(uint64_t descs, int64_t ndesc, int64_t max_rows, int64_t row_bytes, uint64_t stream);
 struct LossDesc {

@@ -14,6 +14,7 @@ input mini-batches (one permutation per epoch, as Keras' joint ``fit`` does: exp
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -33,6 +34,10 @@ class TrainConfig:
     seed: int = 0                     # permutation seed (shared by every organism of a generation)
     max_steps_per_epoch: Optional[int] = None   # CI/debug override only; never used by bench.py
     val_every_epoch: bool = True      # the reference validates after every epoch
+    # Adam moment storage of the HIP engine: "16bit" (bf16 m + log16 v: 16-bit moments as the reference's fp16
+    # floatx keeps them, experiment_worker.py:36-37,80; csrc/hip/common.h MOM_16) or "fp32" (the torch oracle is
+    # always fp32); env SERANN_ADAM_MOMENTS overrides the default
+    adam_moments: str = field(default_factory=lambda: os.environ.get("SERANN_ADAM_MOMENTS", "16bit"))
 
     def split(self, n: int) -> int:
         # keras train_validation_split: split_at = int(floor(n * (1 - validation_split)))

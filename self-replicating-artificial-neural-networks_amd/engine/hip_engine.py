@@ -377,8 +377,10 @@ class HipPopulationEngine(PopulationEngine):
         self.parena = Arena(torch.float32, dev)
         self.sarena = Arena(torch.float32, dev)     # BN moving statistics
         self.layouts: List[OrgLayout] = []
+        org_off = []
         for ir in self.irs:
             lay = OrgLayout(ir)
+            org_off.append(self.parena.size)              # organisms are contiguous in the parameter arena
             for n in ir.nodes:
                 if n.op == "gemm" and n.attrs["kind"] not in ("head_cls", "head_rep"):
                     a = n.attrs
@@ -399,6 +401,11 @@ class HipPopulationEngine(PopulationEngine):
             lay.w[ir.cls_head] = self.parena.alloc((NC + L) * D)
             lay.b[ir.cls_head] = self.parena.alloc(NC + L)
             self.layouts.append(lay)
+        org_off.append(self.parena.size)
+        # divergence flags (csrc/hip/common.h flag_diverged): the Adam passes flag an organism with a gradient
+        # element beyond fp16's range; fit / evaluate report its metrics as NaN
+        self.org_off = torch.as_tensor(np.asarray(org_off, np.int64), device=dev)
+        self.diverged = torch.zeros(max(len(self.irs), 1), dtype=torch.int32, device=dev)
         # transposed bf16 weights for DGRAD (v2): Wt[C][KH][KW][F]
         self.wt_off = []
         wt_size = 0
@@ -418,8 +425,15 @@ class HipPopulationEngine(PopulationEngine):
         self.p = self.parena.materialize()
         # gradients: deterministic Q40 fixed-point accumulator (csrc/hip/common.h fx_*), converted by Adam
         self.g = torch.zeros(self.p.numel(), dtype=torch.int64, device=dev)
-        self.m = torch.zeros_like(self.p)
-        self.v = torch.zeros_like(self.p)
+        # Adam moments: fp32, or 16 bits -- bf16 m, log16 v (TrainConfig.adam_moments; csrc/hip/common.h MOM_16)
+        if self.cfg.adam_moments not in ("16bit", "fp32"):
+            raise ValueError(f"adam_moments must be '16bit' or 'fp32', not {self.cfg.adam_moments!r}")
+        self.mom_mode = H.MOM_16 if self.cfg.adam_moments == "16bit" else H.MOM_F32
+        m16 = self.mom_mode == H.MOM_16
+        self.m = torch.zeros(self.p.numel(), dtype=torch.bfloat16 if m16 else torch.float32, device=dev)
+        # (log16 v: int16 code -32768 is v = 0)
+        self.v = (torch.full((self.p.numel(),), -32768, dtype=torch.int16, device=dev) if m16
+                  else torch.zeros(self.p.numel(), dtype=torch.float32, device=dev))
         self.pbf = torch.zeros(self.p.numel() + SLACK, dtype=torch.bfloat16, device=dev)
         self.stats = self.sarena.materialize()
         self.step_i = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -1655,6 +1669,7 @@ class HipPopulationEngine(PopulationEngine):
         counter = torch.zeros(1, dtype=torch.int32, device=dev)
         metrics = torch.zeros(P, 4, dtype=torch.int64, device=dev)      # Q32 fixed point (aux.hip loss_kernel)
 
+        self.diverged.zero_()                       # (flags of this fit only)
         t_plan = time.perf_counter()
         mem = self._alloc_buffers(B, with_grads=True)
         self.timings["alloc_s"] = time.perf_counter() - t_plan
@@ -1669,7 +1684,8 @@ class HipPopulationEngine(PopulationEngine):
         # does every parameter)
         actx = np.zeros(1, dtype=H.ADAM_CTX_DTYPE)
         actx[0] = (self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(), self.g.data_ptr(),
-                   self.lr_t.data_ptr(), cfg.beta1, cfg.beta2, cfg.eps, 0.0)
+                   self.lr_t.data_ptr(), self.org_off.data_ptr(), self.diverged.data_ptr(), self.num_organisms,
+                   cfg.beta1, cfg.beta2, cfg.eps, self.mom_mode)
         self._adam_ctx = torch.as_tensor(np.frombuffer(actx.tobytes(), dtype=np.uint8).copy(), device=dev)
         actx_ptr = self._adam_ctx.data_ptr() if os.environ.get("SERANN_FUSE_ADAM", "1") != "0" else 0
         plans = [self._build_plan("train", B, mem, inputs, yb.data_ptr(), targets, metrics, orgs=g_, adam_ctx=actx_ptr)
@@ -1767,7 +1783,8 @@ class HipPopulationEngine(PopulationEngine):
             s = H.stream_handle()
             L.adam_update(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                           self.pbf.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), cfg.beta1, cfg.beta2, cfg.eps,
-                          skip.data_ptr() if skip is not None else 0, s)
+                          skip.data_ptr() if skip is not None else 0, s, self.mom_mode, self.org_off.data_ptr(),
+                          self.diverged.data_ptr(), self.num_organisms)
             L.counter_add(counter.data_ptr(), 1, s)
 
         def remainder_step():
@@ -1800,8 +1817,14 @@ class HipPopulationEngine(PopulationEngine):
         self.graph = graph
         # every buffer the captured graph addresses lives as long as the graph does
         self._fit_bufs = (xb, gb, yb, perm_t, counter, metrics, plans, rem["plans"])
+        div = self.diverged_mask()
+        if div.any():
+            # a gradient beyond fp16's range: the reference's float16 graph ends such an organism with NaN weights
+            # and NaN metrics (common.h flag_diverged)
+            train_acc, val_acc, val_mse = (np.where(div, np.nan, a) for a in (train_acc, val_acc, val_mse))
         return FitResult(train_acc, val_acc, val_mse, time.perf_counter() - t0, total,
                          extra={"plan_s": self.timings["plan_s"], "alloc_s": self.timings["alloc_s"],
+                                "diverged": np.flatnonzero(div).tolist(),
                                 "launches_per_step": self.timings["launches_per_step"]})
 
     def _fit_epochs(self, cfg, split, n, steps, full_steps, use_graph, perm_t, counter, metrics, dd, step,
@@ -1893,7 +1916,8 @@ class HipPopulationEngine(PopulationEngine):
         if apply_adam:
             c = self.cfg
             self.lib.adam(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(),
-                          self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), c.lr, c.beta1, c.beta2, c.eps, s)
+                          self.step_i.data_ptr(), self.lr_t.data_ptr(), self.p.numel(), c.lr, c.beta1, c.beta2, c.eps, s,
+                          self.mom_mode)
         torch.cuda.synchronize(dev)
         self._debug_mem = mem
         self._debug_plan = plan                          # (tests inspect its launches)
@@ -1952,7 +1976,12 @@ class HipPopulationEngine(PopulationEngine):
         cfg = cfg or self.cfg
         dd = device_data_for_arrays(x, labels, g, self.device)
         acc, _ = self._evaluate_rows(dd["x"], dd["g"], dd["y"], 0, len(x), cfg)
-        return acc
+        return np.where(self.diverged_mask(), np.nan, acc)
+
+    def diverged_mask(self) -> np.ndarray:
+        """Organisms whose last fit produced a gradient element beyond fp16's range (csrc/hip/common.h
+        flag_diverged): bool [P]."""
+        return self.diverged[:self.num_organisms].cpu().numpy() != 0
 
     def _rep_plan(self, B: int):
         """Forward-only plan of the replication step at batch B, cached per B: per-organism input

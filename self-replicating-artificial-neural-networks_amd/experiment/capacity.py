@@ -36,15 +36,23 @@ def organism_device_bytes(ir, batch: int, replication_batch: int = 0) -> int:
     transposed copy = 24 B per weight.  Activations: bf16 output and bf16 gradient of every node at the
     batch (fused producers never materialise theirs, which this estimate ignores), the uint8 pool
     argmax, fp32 head logits, the split-K FWD workspaces of long-K merged Dense layers (<= 16 fp32
-    slabs of the output).  ``replication_batch``: the forward-only buffers of the replication plan."""
+    slabs of the output), and the fp32 split slabs of every KH x KW > 1 convolution's WGRAD (at most one slab per
+    CONV_WGRAD_MIN_CHUNKS 128-pixel chunks, capped at CONV_WGRAD_MAX_SLAB_MB per layer: ops/hip_ops.py
+    conv_wgrad_splits).  ``replication_batch``: the forward-only buffers of the replication plan."""
+    from ..ops.hip_ops import CONV_WGRAD_MAX_SLAB_MB, CONV_WGRAD_MIN_CHUNKS
     weights = 0
     act = 0
+    slabs = 0
     for n in ir.nodes:
         if n.op == "gemm":
             a = n.attrs
             if a["kind"] in ("head_cls", "head_rep"):
                 continue
             weights += a["f"] * a["kh"] * a["kw"] * a["cin"] + (a["f"] if a["use_bias"] else 0)
+            if a["kh"] * a["kw"] > 1:
+                chunks = -(-batch * math.prod(n.shape[:-1]) // 128)
+                one = 4 * a["f"] * a["kh"] * a["kw"] * (-(-a["cin"] // 8) * 8)
+                slabs += min(CONV_WGRAD_MAX_SLAB_MB << 20, max(1, chunks // CONV_WGRAD_MIN_CHUNKS) * one)
         elif n.op == "bn":
             weights += 4 * n.attrs["channels"]
         if n.op in ("input", "reshape"):
@@ -59,7 +67,7 @@ def organism_device_bytes(ir, batch: int, replication_batch: int = 0) -> int:
     weights += heads + ir.num_classes + ir.genotype_size
     act += 3 * 4 * (ir.num_classes + ir.genotype_size)          # fp32 logits + bf16 dlogits (+ slack)
     per_sample_fwd = sum(2 * math.prod(n.shape) for n in ir.nodes if n.op not in ("input", "reshape"))
-    total = 24 * weights + batch * act + replication_batch * per_sample_fwd
+    total = 24 * weights + batch * act + slabs + replication_batch * per_sample_fwd
     return int(1.25 * total) + (1 << 20)         # allocator rounding, descriptor tables
 
 

@@ -170,10 +170,10 @@ class Experiment:
             record["ranks"] = times.get("ranks", [])
             record["allgather_s"] = round(float(times.get("allgather_s", 0.0)), 5)
             record["allgather_bytes"] = int(times.get("allgather_bytes", 0))
-            if self._comm.world_size > 1:
-                ms = [v for v in times["rank_measured_s"] if v > 0]
-                record["rank_imbalance"] = max(ms) / (sum(ms) / len(ms)) if ms else float("nan")
-                record["rank_factors"] = times["rank_factors"]
+            # max / mean learning seconds over the ranks that trained anything (1.0 at world size 1)
+            ms = [v for v in times["rank_measured_s"] if v > 0]
+            record["rank_imbalance"] = max(ms) / (sum(ms) / len(ms)) if ms else float("nan")
+            record["rank_factors"] = times["rank_factors"]
 
             if len(valid_serann) == 0:
                 self.log("No valid SeRANNs left! stopping...")
@@ -300,7 +300,11 @@ class Experiment:
                     offspring_rows[int(i)] = off[k]
                 times["learning_times"].append(lt)
                 times["replication_times"].append(rt)
-        predicted = [float(sum(plan.costs[j] for j in part)) for part in parts]
+        # the cost model prices one training step (cost_model.organism_time): x steps per generation, so that
+        # predicted_s and measured_s (a shard's learning seconds) are in the same unit
+        spg = getattr(self._worker, "steps_per_generation", None)
+        spg = spg() if callable(spg) else 0
+        predicted = [float(sum(plan.costs[j] for j in part)) * max(spg, 1) for part in parts]
         times["rank_predicted_s"], times["rank_measured_s"] = predicted, measured
         times["rank_factors"] = self._speeds.update(predicted, measured)
         # per-rank load balance and the collective's own cost, for the multi-GPU records (SCALE runs): every

@@ -83,6 +83,14 @@ class ShardWorker:
         self.log = log or (lambda m: print(m, flush=True))
         self.last_waves: List[List[int]] = []        # (introspection: tests, perf log)
 
+    def steps_per_generation(self) -> int:
+        """Training steps of one generation (epochs x steps per epoch of the training split): the factor between
+        the cost model's seconds per step and a shard's learning seconds."""
+        n = int(getattr(self.data, "n_train", 0) or 0)
+        if n <= 0:
+            return 0
+        return int(self.cfg.epochs) * int(self.cfg.steps_per_epoch(self.cfg.split(n)))
+
     def run(self, indices: Sequence[int], ids: Sequence[str], genotypes: np.ndarray, irs: List[OrganismIR],
             num_replications: int, generation: int, random_seed: int,
             positions: Optional[Sequence[int]] = None, n_trainable: Optional[int] = None) -> ShardResult:

@@ -58,7 +58,10 @@ BN_USTAT = 512
 GF_NBNSUM = 512
 GF_NOSTORE = 32
 GF_ADAM = 256
-ADAM_CTX_DTYPE = np.dtype([(f, _I) for f in ['p', 'm', 'v', 'pbf', 'g', 'lr_t']] + [(f, np.float32) for f in ['b1', 'b2', 'eps', 'pad']])
+ADAM_CTX_DTYPE = np.dtype([(f, _I) for f in ['p', 'm', 'v', 'pbf', 'g', 'lr_t', 'org_off', 'diverged', 'norg']]
+                          + [(f, np.float32) for f in ['b1', 'b2', 'eps']]
+                          + [("mode", np.int32)])
+MOM_F32, MOM_16 = 0, 1            # AdamCtx.mode: fp32 moments, or bf16 m + log16 v (csrc/hip/common.h)
 MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 ACT_CODES = {"linear": 0, "relu": 1, "sigmoid": 2}
 
@@ -191,6 +194,17 @@ def to_qg(t):
 def from_qg(t):
     """int64 gradient-arena tensor (device or host) -> float32 torch tensor on the same device."""
     return (t.double() / QG).float()
+
+
+def moments_f32(m, v) -> tuple:
+    """The Adam moment arenas as fp32 tensors, whatever their storage (csrc/hip/common.h MOM_*): fp32 as is,
+    bf16 m widened, log16 v (int16 q: v = 2^(q / 1024), q = -32768: 0) decoded."""
+    import torch
+    if v.dtype == torch.int16:
+        vf = torch.exp2(v.float() / 1024.0)
+        vf = torch.where(v == -32768, torch.zeros_like(vf), vf)
+        return m.float(), vf
+    return m.float(), v.float()
 
 
 def from_q32(t) -> np.ndarray:

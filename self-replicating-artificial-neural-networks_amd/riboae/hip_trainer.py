@@ -132,7 +132,7 @@ class HipRiboTrainer:
         self.lr_t = torch.zeros(1, dtype=torch.float32, device=dev)
         actx = np.zeros(1, dtype=H.ADAM_CTX_DTYPE)
         actx[0] = (self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.pbf.data_ptr(), self.g.data_ptr(),
-                   self.lr_t.data_ptr(), self.b1, self.b2, self.eps, 0.0)
+                   self.lr_t.data_ptr(), 0, 0, 0, self.b1, self.b2, self.eps, H.MOM_F32)
         self._adam_ctx = torch.as_tensor(np.frombuffer(actx.tobytes(), dtype=np.uint8).copy(), device=dev)
         with torch.no_grad():
             for name, mod, attr, klayout, perm in self.specs:

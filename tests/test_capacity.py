@@ -247,3 +247,31 @@ def test_collective_timeout_follows_job_timeout(monkeypatch):
     from serann.parallel.comm import collective_timeout_s
     monkeypatch.setitem(experiment_config, "worker_pool_job_timeout", 100)
     assert collective_timeout_s() == 400.0
+
+
+def test_device_bytes_cover_conv_wgrad_slabs():
+    """Split conv WGRADs allocate fp32 slabs (ops/hip_ops.py conv_wgrad_splits, ``_wgfin``): the estimate counts
+    at least the slab bytes the planner gives an organism's KxK convolutions at the production batch."""
+    from serann.ops import hip_ops as H
+    ir = interpret("X_layer = Conv2D(filters=32, kernel_size=3, strides=1)(X_layer)\n"
+                   "X_layer = Conv2D(filters=32, kernel_size=3, strides=1)(X_layer)\n\n"
+                   "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+                   "con = Dense(units=64, activation='relu')(con)\n\nloss_balance = 0.5")
+    B = 750
+    slab = 0
+    for n in ir.nodes:
+        if n.op != "gemm" or n.attrs["kh"] * n.attrs["kw"] <= 1:
+            continue
+        a = n.attrs
+        (Hh, Ww, C), (OH, OW, F) = ir.node(n.inputs[0]).shape, n.shape
+        row = dict(a=0, b=0, out=1, H=Hh, W=Ww, C=C, OH=OH, OW=OW, F=F, KH=a["kh"], KW=a["kw"], SH=1, SW=1, M=F,
+                   N=a["kh"] * a["kw"] * C, K=B * OH * OW, flags=0)
+        for _, rws, _ in H.gemm3_plan(H.MODE_WGRAD, [row], [(F, row["N"], row["K"])]):
+            if rws[0].get("_wgfin"):
+                slab += 4 * H.wgrad_slab_elems(rws[0])
+    assert slab > 0
+    with_slabs = capacity.organism_device_bytes(ir, B)
+    # the same organism's estimate without the convolutions' slabs (the old formula) would miss them
+    assert with_slabs >= slab + 24 * sum(n.attrs["f"] * n.attrs["kh"] * n.attrs["kw"] * n.attrs["cin"]
+                                         for n in ir.nodes if n.op == "gemm" and n.attrs["kind"] not in
+                                         ("head_cls", "head_rep"))

@@ -80,6 +80,18 @@ def test_gloo_world_matches_world1(tmp_path, world):
         assert sum(r["organisms"] for r in ranks) == rec["valid"]
         assert all(r["shard_s"] >= r["measured_s"] >= 0 and r["predicted_s"] >= 0 for r in ranks)
         assert rec["allgather_s"] > 0 and rec["allgather_bytes"] > 0
+        assert rec["rank_imbalance"] >= 1.0 and len(rec["rank_factors"]) == world
+    # predicted_s is in the unit of measured_s (learning seconds of the generation): the cost model's seconds per
+    # step of every trained organism times the generation's steps (1 epoch x ceil(950 / 250))
+    from serann.experiment.cost_model import organism_time
+    from serann.genome.interpreter import interpret
+    con = sqlite3.connect(p2)
+    for rec in recs:
+        rows = con.execute("select source_code from serann where generation = ? and is_valid = 1 and "
+                           "is_overweight = 0", (rec["generation"],)).fetchall()
+        want = 4 * sum(organism_time(interpret(r[0])) for r in rows)
+        got = sum(r["predicted_s"] for r in rec["ranks"])
+        assert abs(got - want) <= 1e-3 * want + 1e-4 * world, (got, want)
 
 
 def test_rank_speed_model_balances_injected_slowdowns():

@@ -171,10 +171,11 @@ def test_fit_is_bitwise_reproducible():
     assert np.array_equal(r0.val_mse, r1.val_mse)
 
 
-def test_fused_adam_matches_the_arena_pass(monkeypatch):
+@pytest.mark.parametrize("moments", ["16bit", "fp32"])
+def test_fused_adam_matches_the_arena_pass(moments, monkeypatch):
     """WGRAD tiles with a single writer apply Adam in their epilogue (GF_ADAM) and the arena-wide pass skips
     them: after a 2-epoch fit (graph replay, remainder step) weights, moments and bf16 copies are bitwise
-    those of the arena pass over every parameter."""
+    those of the arena pass over every parameter, with either moment storage."""
     from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
     from serann.engine.base import TrainConfig
     from serann.engine.hip_engine import HipPopulationEngine
@@ -182,7 +183,7 @@ def test_fused_adam_matches_the_arena_pass(monkeypatch):
                            n_train=2200, n_test=300)
     names = sorted(ARCHS)
     irs = [interpret(ARCHS[n]) for n in names]
-    cfg = TrainConfig(epochs=2, batch_size=256)
+    cfg = TrainConfig(epochs=2, batch_size=256, adam_moments=moments)
     out = []
     for fuse in ("1", "0"):
         monkeypatch.setenv("SERANN_FUSE_ADAM", fuse)
@@ -193,7 +194,7 @@ def test_fused_adam_matches_the_arena_pass(monkeypatch):
     (p1, m1, v1, b1, r1, sk1), (p0, m0, v0, b0, r0, sk0) = out
     assert sk1[0] is not None and int((sk1[0] != 0).sum()) > 0       # some tiles were fused
     assert sk0[0] is None
-    diffs = {k: float((a - b).abs().max()) for k, a, b in (("p", p1, p0), ("m", m1, m0), ("v", v1, v0))}
+    diffs = {k: float((a.float() - b.float()).abs().max()) for k, a, b in (("p", p1, p0), ("m", m1, m0), ("v", v1, v0))}
     assert torch.equal(p1, p0) and torch.equal(m1, m0) and torch.equal(v1, v0) and torch.equal(b1, b0), diffs
     assert np.array_equal(r1.val_acc, r0.val_acc)
 
@@ -536,3 +537,112 @@ def test_adam_kernel_matches_keras_formula():
     assert torch.all(g == 0)
     assert int(step.item()) == 1
     assert torch.allclose(pbf.float(), ref, atol=1e-2, rtol=1e-2)
+
+
+def _adam_run(mode, steps, grads, p0):
+    """``steps`` arena Adam steps (hip adam kernel, moment storage ``mode``) on the gradient sequence ``grads``."""
+    from serann.ops import hip_ops as H
+    lib = H.lib()
+    n = p0.numel()
+    p = p0.clone()
+    m16 = mode == H.MOM_16
+    m = torch.zeros(n, dtype=torch.bfloat16 if m16 else torch.float32, device="cuda")
+    v = (torch.full((n,), -32768, dtype=torch.int16, device="cuda") if m16
+         else torch.zeros(n, dtype=torch.float32, device="cuda"))
+    pbf = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+    step = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lr_t = torch.zeros(1, device="cuda")
+    for t in range(steps):
+        g = H.to_qg(grads(t))
+        lib.adam(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), pbf.data_ptr(), step.data_ptr(),
+                 lr_t.data_ptr(), n, 1e-3, 0.9, 0.999, 1e-4, H.stream_handle(), mode)
+    torch.cuda.synchronize()
+    return p, m, v
+
+
+def test_adam_16bit_moments_track_fp32_moments():
+    """bf16 m + log16 v (csrc/hip/common.h MOM_16) against fp32 moments over a generation's 380 steps of noisy
+    gradients whose scales span 1e-7 .. 10 (the eps = 1e-4 regime and above): the parameter displacement of each
+    element stays within a few percent of the fp32-moment run, and the moments decode to the fp32 moments."""
+    from serann.ops import hip_ops as H
+    n = 4096
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    scale = 10.0 ** torch.empty(n, device="cuda").uniform_(-7, 1, generator=gen)
+    bias = torch.randn(n, device="cuda", generator=gen)
+    p0 = torch.randn(n, device="cuda", generator=gen)
+    noise = torch.randn(380, n, device="cuda", generator=gen)
+
+    def grads(t):
+        return scale * (0.5 * bias + noise[t])
+    p32, m32, v32 = _adam_run(H.MOM_F32, 380, grads, p0)
+    p16, m16, v16 = _adam_run(H.MOM_16, 380, grads, p0)
+    d32, d16 = p32 - p0, p16 - p0
+    rel = (d16 - d32).abs() / d32.abs().clamp_min(1e-12)
+    big = d32.abs() > 1e-6                        # displacements that are not ~0 (every scale >= ~1e-6)
+    # elements whose noisy updates nearly cancel (a random walk back to ~0) are measured against 5 % of the
+    # largest path an Adam step sequence can take (~ lr per step)
+    rel_path = (d16 - d32).abs() / (d32.abs() + 0.05 * 380 * 1e-3)
+    stats = dict(median=float(rel[big].median()), q99_path=float(torch.quantile(rel_path, 0.99)),
+                 norm=float((d16 - d32).norm() / d32.norm()))
+    assert stats["median"] < 0.01 and stats["q99_path"] < 0.05 and stats["norm"] < 0.02, stats
+    mf, vf = H.moments_f32(m16, v16)
+    live = v32 > 2.0 ** -30
+    assert float(((vf - v32).abs() / v32)[live].max()) < 0.03
+    mrel = (mf - m32).abs() / m32.abs().clamp_min(1e-30)
+    assert float(mrel[m32.abs() > 1e-3 * m32.abs().max()].median()) < 0.01
+
+
+def test_fit_16bit_moments_vs_fp32_moments():
+    """A 2-epoch fit (>= 50 graph-replayed Adam steps, 4 stream groups, fused-Adam WGRAD epilogues) with 16-bit
+    moments against the same fit with fp32 moments: weight displacements agree to a few percent of their size and
+    the validation accuracies to 0.05 (the reference itself keeps fp16 moments)."""
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=8000, n_test=500, seed=12),
+                           n_train=8000, n_test=500)
+    names = sorted(ARCHS)
+    irs = [interpret(ARCHS[n]) for n in names]
+    runs = {}
+    for mode in ("fp32", "16bit"):
+        cfg = TrainConfig(epochs=2, batch_size=256, adam_moments=mode)
+        eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
+        p0 = eng.p.clone()
+        res = eng.fit(data, cfg)
+        assert res.steps >= 50
+        runs[mode] = (eng.p - p0, res, [eng.export_arena(i, eng.p - p0) for i in range(len(irs))])
+        assert (eng.m.dtype == torch.bfloat16) == (mode == "16bit")
+        del eng
+    d32, r32, e32 = runs["fp32"]
+    d16, r16, e16 = runs["16bit"]
+    assert np.all(np.abs(r16.val_acc - r32.val_acc) < 0.05), (r16.val_acc, r32.val_acc)
+    for i, name in enumerate(names):
+        keys = [(k, w) for k in e32[i] for w in e32[i][k] if not w.startswith("moving")]
+        num = sum(float(np.linalg.norm(e16[i][k][w] - e32[i][k][w])) ** 2 for k, w in keys)
+        den = sum(float(np.linalg.norm(e32[i][k][w])) ** 2 for k, w in keys)
+        assert num ** 0.5 < 0.1 * den ** 0.5 + 1e-6, (name, num ** 0.5, den ** 0.5)
+
+
+def test_exploding_organism_is_flagged_diverged():
+    """An organism whose gradients leave fp16's range (weights scaled x1000 per layer: activations ~1e9) is flagged
+    by the Adam passes (csrc/hip/common.h flag_diverged) and its metrics come back NaN -- the reference's float16
+    graph turns it into NaN weights -- while its neighbour in the same shard trains normally."""
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=1500, n_test=300, seed=13),
+                           n_train=1500, n_test=300)
+    names = ("conv_pool_dense", "empty_x_branch")
+    irs = [interpret(ARCHS[n]) for n in names]
+    params = [init_params(ir, 7 + i) for i, ir in enumerate(irs)]
+    for nid in params[1]:
+        if "kernel" in params[1][nid]:
+            params[1][nid]["kernel"] = params[1][nid]["kernel"] * 1000.0
+    cfg = TrainConfig(epochs=1, batch_size=250)
+    eng = HipPopulationEngine(irs, [0, 1], device="cuda", cfg=cfg, params=params)
+    res = eng.fit(data, cfg)
+    assert res.extra["diverged"] == [1], res.extra["diverged"]
+    assert np.isfinite(res.val_acc[0]) and np.isnan(res.val_acc[1]) and np.isnan(res.val_mse[1])
+    acc = eng.evaluate(data.test_x, data.test_labels, data.test_g, cfg)
+    assert np.isfinite(acc[0]) and np.isnan(acc[1])
+    eng.close()
