@@ -42,6 +42,8 @@ def main():
                     help="write the source codes of the last generation (JSON list) for scripts/bench_step.py")
     ap.add_argument("--profile-dir", default=None,
                     help="torch.profiler Chrome trace of the run per rank (diagnostics; not a headline timing)")
+    ap.add_argument("--no-fixed-pop", action="store_true",
+                    help="skip the fixed-population step timings printed after the timed generations")
     args = ap.parse_args()
 
     import numpy as np
@@ -103,6 +105,13 @@ def main():
     k = len(timed)
     elapsed = t1 - marks.get("t0", t1)
     elapsed = comm.allreduce_max(elapsed)
+    # Fixed-population step times (after the timed region, rank 0 only): the evolved trajectory -- and with it the
+    # work of a generation -- moves with every rounding or data change, so kernel progress across trees is read
+    # from two fixed populations instead: ms per captured-graph training step at 4 stream groups, batch 750
+    fixed = None
+    if comm.is_root and is_cuda and s.engine == "hip" and not args.no_fixed_pop:
+        fixed = fixed_population_ms(s.data)
+    comm.barrier()
     if comm.is_root:
         sec_per_gen = elapsed / max(k, 1)
         value = pop * k / elapsed if elapsed > 0 and k else 0.0
@@ -135,6 +144,9 @@ def main():
             if timed else None,
             "achieved_model_tflops": (sum(h.get("train_tflop", 0.0) for h in timed) / elapsed)
             if elapsed > 0 and timed else None,        # (train_tflop counts the whole population)
+            # trajectory-independent kernel progress: populations/*.json, 4 stream groups, graph replay (not timed
+            # above; measured after the K generations)
+            "fixed_pop_ms_per_step": fixed,
         }
         print(json.dumps(out), flush=True)
     if comm.is_root and args.dump_population and db is not None:
@@ -145,6 +157,38 @@ def main():
         with open(args.dump_population, "w") as f:
             json.dump([r[0] for r in rows], f)
     comm.shutdown()
+
+
+def fixed_population_ms(data, streams: int = 4, steps: int = 60) -> dict:
+    """ms per replayed training step (batch 750, ``streams`` stream groups) of the two fixed populations in
+    populations/: the generation-3 mix of the bench trajectory (106 organisms) and 125 clones of the example.json
+    ancestor (scripts/bench_step.py measures the same)."""
+    import torch
+    from serann.engine.base import TrainConfig
+    from serann.engine.hip_engine import HipPopulationEngine
+    from serann.genome.interpreter import try_interpret
+    out = {}
+    root = os.path.dirname(os.path.abspath(__file__))
+    saved = os.environ.get("SERANN_STREAMS")
+    os.environ["SERANN_STREAMS"] = str(streams)
+    try:
+        for name in ("bench_gen3_pop125", "ancestor_pop125"):
+            with open(os.path.join(root, "populations", f"{name}.json")) as f:
+                irs = [try_interpret(src).ir for src in json.load(f)][:125]
+            cfg = TrainConfig(epochs=1, batch_size=750, val_every_epoch=False, max_steps_per_epoch=steps)
+            eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
+            eng.fit(data, cfg)
+            torch.cuda.synchronize()
+            out[name] = round(float(eng.timings.get("replay_ms_per_step", float("nan"))), 3)
+            eng.close()
+            del eng
+    finally:
+        if saved is None:
+            os.environ.pop("SERANN_STREAMS", None)
+        else:
+            os.environ["SERANN_STREAMS"] = saved
+    out["streams"] = streams
+    return out
 
 
 if __name__ == "__main__":

@@ -57,6 +57,9 @@ def _hipcc():
 # gchain.hip keeps its MFMA accumulators in VGPRs: they are read by VALU epilogues every tile, and the
 # AGPR form costs a v_accvgpr_read per element
 PER_FILE_FLAGS = {"gchain.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# sources compiled as several objects (-D<macro>=0..n-1), each instantiating a part of the kernels: gemm3.hip's
+# launcher is split in four (its template instantiations are most of the build time)
+MULTI_PART = {"gemm3.hip": ("GEMM3_PART", 4)}
 
 
 def build_hip(jobs: int = 4):
@@ -78,9 +81,21 @@ def build_hip(jobs: int = 4):
     stamp = build_dir / "src_hash.txt"
     stale_digest = not stamp.exists() or stamp.read_text().strip() != digest
 
-    def compile_one(src):
-        obj = build_dir / (src.stem + ".o")
-        extra = PER_FILE_FLAGS.get(src.name, [])
+    units = []
+    for src in srcs:
+        if src.name in MULTI_PART:
+            macro, n = MULTI_PART[src.name]
+            units += [(src, f"{src.stem}_p{i}", [f"-D{macro}={i}"]) for i in range(n)]
+        else:
+            units.append((src, src.stem, []))
+    for stale in build_dir.glob("*.o"):           # objects of a former unit layout
+        if stale.stem not in {u[1] for u in units}:
+            stale.unlink()
+
+    def compile_one(unit):
+        src, stem, defs = unit
+        obj = build_dir / (stem + ".o")
+        extra = PER_FILE_FLAGS.get(src.name, []) + defs
         if src.name == "module.hip":
             extra = extra + [f'-DSERANN_SRC_HASH="{digest}"']
         # incremental: an object newer than its source and every header is reused
@@ -90,8 +105,10 @@ def build_hip(jobs: int = 4):
         _run([hipcc, *flags, *extra, "-c", str(src), "-o", str(obj)])
         return obj
 
+    # heaviest units first, so the pool does not end on one long compile
+    units.sort(key=lambda u: -u[0].stat().st_size)
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(compile_one, srcs))
+        objs = list(ex.map(compile_one, units))
     out = NATIVE / f"serann_hip{_ext_suffix()}"
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", *map(str, objs), "-o", str(out)])
     stamp.write_text(digest)

@@ -155,21 +155,25 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // as the reference keeps them (fp16 floatx: experiment_worker.py:36-37, optimizer :80), master weights fp32:
 //  * m: bf16 (RNE).  b1 = 0.9 moves m by 10 % of (g - m) per step, far above bf16's half ulp (2^-9), so the EMA
 //    tracks; the stored value carries 0.4 % relative error into the update.
-//  * v: "log16", q = rint(1024 log2 v) as int16 (q = -32768: v = 0; v < 2^-32 flushes to 0, v > 2^32 saturates).
-//    An EMA with b2 = 0.999 moves v by 0.1 % of (g^2 - v) per step: in bf16 (half ulp 0.2 %) that increment rounds
-//    away unless g^2 > 3 v, so v would freeze.  log16's adjacent values differ by 2^(1/1024) (half ulp 0.034 %, fp16's
-//    relative precision) over 2^-32 .. 2^32 -- fp16 itself flushes v below 6e-8 (|g| < 2.4e-4) and overflows at
-//    65504.  sqrt(v) = 2^(q / 2048) is what the update reads.
+//  * v: "log16", an unsigned 16-bit log code: q = rint(LOG16_SCALE * (log2 v + LOG16_BIAS)) in [1, 65535] covers
+//    v in [2^-48, 2^32) = [3.6e-15, 4.3e9] (80 octaves, 819.2 codes per octave); q = 0 is v = 0, and v < 2^-48 flushes
+//    to 0 (sqrt(v) < 6e-8, nothing next to eps = 1e-4), v >= 2^32 saturates (|g| > 65504: flag_diverged).  An EMA
+//    with b2 = 0.999 moves v by 0.1 % of (g^2 - v) per step: in bf16 (half ulp 0.2 %) that increment rounds away
+//    unless g^2 > 3 v, so v would freeze.  log16's neighbouring values differ by 2^(1/819.2) (half ulp 0.042 %,
+//    within fp16's 0.024 .. 0.049 %), over a range fp16 lacks: fp16 flushes v below 6e-8 (|g| < 2.4e-4) and
+//    overflows at 65504.  sqrt(v) is what the update reads.
 // The arithmetic is adam_elem's in fp32 either way; the moments are rounded once when stored.  18 B per parameter
 // and step instead of 26 in the fused WGRAD epilogues (p 4+4, m 2+2, v 2+2, bf16 shadow 2).
 constexpr int MOM_F32 = 0, MOM_16 = 1;
-__device__ __forceinline__ float log16_f(int16_t q) {
-    return q == (int16_t)-32768 ? 0.f : __builtin_amdgcn_exp2f((float)q * (1.f / 1024.f));
+constexpr float LOG16_SCALE = 819.2f, LOG16_BIAS = 48.f;
+__device__ __forceinline__ float log16_f(uint32_t q) {          // q: the low 16 bits are the code
+    q &= 0xffffu;
+    return q == 0 ? 0.f : __builtin_amdgcn_exp2f((float)q * (1.f / LOG16_SCALE) - LOG16_BIAS);
 }
-__device__ __forceinline__ int16_t log16_q(float v) {
-    if (!(v >= 2.3283064e-10f)) return (int16_t)-32768;          // 0, < 2^-32 (and NaN, never produced)
-    const float l = fminf(__builtin_amdgcn_logf(v) * 1024.f, 32767.f);
-    return (int16_t)__float2int_rn(l);
+__device__ __forceinline__ uint16_t log16_q(float v) {
+    if (!(v >= 3.5527137e-15f)) return 0;                           // 0, < 2^-48 (and NaN, never produced)
+    const float l = (__builtin_amdgcn_logf(v) + LOG16_BIAS) * LOG16_SCALE;
+    return (uint16_t)min(max(__float2int_rn(l), 1), 65535);
 }
 template <int MM>
 __device__ __forceinline__ float m_ld(const void* b, int64_t e) {
@@ -183,12 +187,12 @@ __device__ __forceinline__ void m_st(void* b, int64_t e, float x) {
 }
 template <int MM>
 __device__ __forceinline__ float v_ld(const void* b, int64_t e) {
-    if constexpr (MM == MOM_16) return log16_f(reinterpret_cast<const int16_t*>(b)[e]);
+    if constexpr (MM == MOM_16) return log16_f(reinterpret_cast<const uint16_t*>(b)[e]);
     else return reinterpret_cast<const float*>(b)[e];
 }
 template <int MM>
 __device__ __forceinline__ void v_st(void* b, int64_t e, float x) {
-    if constexpr (MM == MOM_16) reinterpret_cast<int16_t*>(b)[e] = log16_q(x);
+    if constexpr (MM == MOM_16) reinterpret_cast<uint16_t*>(b)[e] = log16_q(x);
     else reinterpret_cast<float*>(b)[e] = x;
 }
 // four consecutive moments, e % 4 == 0 (16-B fp32 / 8-B 16-bit vectors)
@@ -212,8 +216,8 @@ __device__ __forceinline__ void m_st4(void* b, int64_t e, float4 x) {
 template <int MM>
 __device__ __forceinline__ float4 v_ld4(const void* b, int64_t e) {
     if constexpr (MM == MOM_16) {
-        const short4 q = *reinterpret_cast<const short4*>(reinterpret_cast<const int16_t*>(b) + e);
-        return make_float4(log16_f(q.x), log16_f(q.y), log16_f(q.z), log16_f(q.w));
+        const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(b) + e);
+        return make_float4(log16_f(q.x), log16_f(q.x >> 16), log16_f(q.y), log16_f(q.y >> 16));
     } else {
         return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(b) + e);
     }
@@ -221,8 +225,9 @@ __device__ __forceinline__ float4 v_ld4(const void* b, int64_t e) {
 template <int MM>
 __device__ __forceinline__ void v_st4(void* b, int64_t e, float4 x) {
     if constexpr (MM == MOM_16)
-        *reinterpret_cast<short4*>(reinterpret_cast<int16_t*>(b) + e) =
-            make_short4(log16_q(x.x), log16_q(x.y), log16_q(x.z), log16_q(x.w));
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(b) + e) =
+            make_uint2((uint32_t)log16_q(x.x) | ((uint32_t)log16_q(x.y) << 16),
+                       (uint32_t)log16_q(x.z) | ((uint32_t)log16_q(x.w) << 16));
     else
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(b) + e) = x;
 }

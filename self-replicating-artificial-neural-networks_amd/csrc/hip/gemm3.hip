@@ -640,32 +640,13 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
         // p / m / v / pbf as 64-B quarter rows, one element per lane per instruction.  Staged, a lane takes 4
         // consecutive columns of one row: 16-B accesses, whole 256-B row segments per 16 lanes, a quarter of the
         // memory instructions.  Two rounds of two waves (the LDS holds two wave tiles).
-        // Every wave issues the p / m / v loads of all its NIT row passes first, before the two LDS rounds: one
-        // memory round trip per wave instead of NIT serial ones (a pass's loads could not move above the previous
-        // pass's stores through possibly aliasing pointers), and the second round's loads fly during the first.
-        constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG, NIT = TR / RPI;
-        using MT = typename std::conditional<MM == MOM_16, uint2, float4>::type;
+        constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG;
         const int64_t t0 = e0 + (int64_t)frow0 * ldo + kcol0;
         const bool vec = (t0 & 3) == 0 && (ldo & 3) == 0;      // float4-aligned rows
         const int cg = lane % CG, rr = lane / CG;
         const int col = kcol0 + cg * 4;
-        float4 pr[NIT];
-        MT mr[NIT], vr[NIT];
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int row = frow0 + it * RPI + rr;
-            if (vec && row < g.M && col + 4 <= g.N) {
-                const int64_t e = e0 + (int64_t)row * ldo + col;
-                pr[it] = *reinterpret_cast<const float4*>(&P[e]);
-                if constexpr (MM == MOM_16) {
-                    mr[it] = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(Mo) + e);
-                    vr[it] = *reinterpret_cast<const uint2*>(reinterpret_cast<const int16_t*>(Vo) + e);
-                } else {
-                    mr[it] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Mo) + e);
-                    vr[it] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Vo) + e);
-                }
-            }
-        }
+        // (issuing every pass's p / m / v loads ahead of the LDS rounds -- one round trip instead of TR / RPI --
+        // measured 30 % slower on the ancestor step: the prefetch registers cost the k loop its occupancy)
         for (int half = 0; half < 2; ++half) {
             __syncthreads();
             if ((wave >> 1) == half) {
@@ -679,26 +660,16 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int it = 0; it < NIT; ++it) {
+                for (int it = 0; it < TR / RPI; ++it) {
                     const int row = frow0 + it * RPI + rr;
                     if (row >= g.M || col >= g.N) continue;
                     const float4 gv = *reinterpret_cast<const float4*>(&st[(it * RPI + rr) * LD + cg * 4]);
                     const int64_t e = e0 + (int64_t)row * ldo + col;
                     chk(fmaxf(fmaxf(fabsf(gv.x), fabsf(gv.y)), fmaxf(fabsf(gv.z), fabsf(gv.w))), e);
                     if (vec && col + 4 <= g.N) {
-                        float4 p4 = pr[it], m4, v4;
-                        if constexpr (MM == MOM_16) {
-                            const uint2 u = mr[it];
-                            m4 = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                             __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-                            const uint2 w = vr[it];
-                            v4 = make_float4(log16_f((int16_t)(w.x & 0xffffu)), log16_f((int16_t)(w.x >> 16)),
-                                             log16_f((int16_t)(w.y & 0xffffu)), log16_f((int16_t)(w.y >> 16)));
-                        } else {
-                            m4 = mr[it];
-                            v4 = vr[it];
-                        }
+                        float4 p4 = *reinterpret_cast<const float4*>(&P[e]);
+                        float4 m4 = m_ld4<MM>(Mo, e);
+                        float4 v4 = v_ld4<MM>(Vo, e);
                         adam_elem(p4.x, m4.x, v4.x, fx_f(fx_q(gv.x)), lr_t, ac.b1, ac.b2, ac.eps);
                         adam_elem(p4.y, m4.y, v4.y, fx_f(fx_q(gv.y)), lr_t, ac.b1, ac.b2, ac.eps);
                         adam_elem(p4.z, m4.z, v4.z, fx_f(fx_q(gv.z)), lr_t, ac.b1, ac.b2, ac.eps);
@@ -763,7 +734,8 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
 
 template <int TF, int TK>
 __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x4_t (&acc)[TF][TK], int frow0,
-                                            int kcol0, int lane, float* stage = nullptr, int wave = 0) {
+                                            int kcol0, int lane, float* stage = nullptr, int wave = 0,
+                                            float* slab = nullptr) {
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     long long* out = reinterpret_cast<long long*>(d.out);     // Q40 gradient arena (common.h fx_*)
     const int ldo = d.ldo ? (int)d.ldo : g.N;        // output row stride (a column slice of a wider dW)
@@ -774,8 +746,8 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
             wgrad_adam_flush<MOM_F32, TF, TK>(d, g, acc, frow0, kcol0, lane, stage, wave);
         return;
     }
-    if (stage != nullptr && (g.flags & GF_WSTORE)) {
-        // sole writer, plain stores: row-major through LDS as the Adam path above, a lane storing 4 consecutive
+    if (stage != nullptr && (slab != nullptr || (g.flags & GF_WSTORE))) {
+        // sole writer (of the Q40 tile, or of this split's fp32 slab tile), plain stores: row-major through LDS as the Adam path above, a lane storing 4 consecutive
         // Q40 elements of a row (two 16-B stores) instead of one 8-B element of 4 rows x 1 column
         constexpr int TR = TF * 16, TC = TK * 16, LD = TC + 4, CG = TC / 4, RPI = 64 / CG;
         const bool vec = (reinterpret_cast<uintptr_t>(out + (int64_t)frow0 * ldo + kcol0) & 15) == 0 && (ldo & 1) == 0;
@@ -797,6 +769,18 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
                     const int row = frow0 + r0 + rr, col = kcol0 + cg * 4;
                     if (row >= g.M || col >= g.N) continue;
                     const float4 gv = *reinterpret_cast<const float4*>(&st[(r0 + rr) * LD + cg * 4]);
+                    if (slab != nullptr) {
+                        float* o = slab + (int64_t)row * g.N + col;
+                        if ((g.N & 3) == 0 && col + 4 <= g.N) {
+                            *reinterpret_cast<float4*>(o) = gv;
+                        } else {
+                            const float gq[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                if (col + q < g.N) o[q] = gq[q];
+                        }
+                        continue;
+                    }
                     long long* o = out + (int64_t)row * ldo + col;
                     if (vec && col + 4 <= g.N) {
                         typedef long long ll2 __attribute__((ext_vector_type(2)));
@@ -823,8 +807,10 @@ __device__ __forceinline__ void wgrad_flush(const GemmDesc& d, const G3& g, f32x
             for (int r = 0; r < 4; ++r) {
                 const int row = frow0 + i * 16 + rq + r;
                 if (row < g.M) {
-                    // GF_WSTORE: this block is the problem's only m-split -> the sole writer
-                    if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = fx_q(acc[i][j][r]);
+                    // GF_WSLAB: m-split -> this split's fp32 slab (plain stores; wgrad_finalize sums the splits in
+                    // order); GF_WSTORE: this block is the problem's only m-split -> the sole writer
+                    if (slab != nullptr) slab[(int64_t)row * g.N + col] = acc[i][j][r];
+                    else if (g.flags & GF_WSTORE) out[(int64_t)row * ldo + col] = fx_q(acc[i][j][r]);
                     else fx_add(out + (int64_t)row * ldo + col, acc[i][j][r]);
                 }
             }
@@ -1107,8 +1093,11 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
     }
     // (the fused-Adam epilogue stages through the LDS tiles when two wave tiles of fp32 fit in them)
     constexpr bool ADAM_STAGE = RG == 1 && NWV == 4 && 2 * (TF * 16) * (TK * 16 + 4) * 4 <= SMEM * 2;
+    // GF_WSLAB (m-split): split kt0 / kper's fp32 slab [M][N] at ext (serann_hip.h GF_WSLAB)
+    float* slab = (d.flags & GF_WSLAB) ? reinterpret_cast<float*>(d.ext) + (int64_t)(kt0 / (int)d.kper) * g.M * g.N
+                                       : nullptr;
     wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane,
-                        ADAM_STAGE ? reinterpret_cast<float*>(smem) : nullptr, wave);
+                        ADAM_STAGE ? reinterpret_cast<float*>(smem) : nullptr, wave, slab);
 }
 
 // ==================================================================================================
@@ -1274,7 +1263,9 @@ __global__ __launch_bounds__(256) void g3_dwgrad_kernel(const GemmDesc* __restri
             if (lane < 16 && f < g.F) fx_add(dbias + f, bsum[i]);
         }
     }
-    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane);
+    float* slab = (d.flags & GF_WSLAB) ? reinterpret_cast<float*>(d.ext) + (int64_t)(kt0 / (int)d.kper) * g.M * g.N
+                                       : nullptr;
+    wgrad_flush<TF, TK>(d, g, acc, f0 + wf * (BMF / WR), k0c + wk * (BNK / WC), lane, nullptr, 0, slab);
 }
 
 // ==================================================================================================
@@ -2755,20 +2746,29 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
 //                 LDS-halo conv WGRAD: 3000000 + 100000 * patch tier + BMF * 1000 + BNK / 64 (column tiles per wave:
 //                 2 .. 32);
 //                 tiles (prob, ftile << 16 | ktile, chunk0, chunk1)
-void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
-    if (ntiles <= 0) return;
-    hipStream_t s = as_stream(stream);
-    const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
-    const int4* tp = as_ptr<const int4>(tiles);
-    dim3 grid((unsigned)ntiles), block(256);
+// The launcher is compiled in four parts (GEMM3_PART = 0..3, one object each, built in parallel: serann/build.py
+// MULTI_PART); every part instantiates only the kernels its variants launch.  GEMM3_PART undefined: all parts here.
+#ifndef GEMM3_PART
+#define GEMM3_PART -1
+#endif
+#define G3_PART(k) (GEMM3_PART < 0 || GEMM3_PART == (k))
+bool gemm3_launch_part0(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp, const int4* tp);
+bool gemm3_launch_part1(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp, const int4* tp);
+bool gemm3_launch_part2(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp, const int4* tp);
+bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp, const int4* tp);
+
+#if G3_PART(0)
+// part 0: Dense / 1x1 and narrow WGRAD
+bool gemm3_launch_part0(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
+                          const int4* tp) {
     if (mode == MODE_WGRAD && variant >= 5000000) {
         // LDS-DMA Dense / 1x1 WGRAD: 5000000 + BMF * 1000 + BNK (+ 500: act' from a staged Y tile)
         const int v = variant - 5000000;
 #define DW3(BMF_, BNK_)                                                                                  \
     if (v == BMF_ * 1000 + BNK_) { hipLaunchKernelGGL((g3_dwgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
-                                   SERANN_CHECK(hipGetLastError()); return; }                            \
+                                   SERANN_CHECK(hipGetLastError()); return true; }                            \
     if (v == BMF_ * 1000 + BNK_ + 500) { hipLaunchKernelGGL((g3_dwgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
-                                         SERANN_CHECK(hipGetLastError()); return; }
+                                         SERANN_CHECK(hipGetLastError()); return true; }
         DW3(64, 128) DW3(64, 64) DW3(32, 128) DW3(32, 64) DW3(16, 256) DW3(16, 128) DW3(16, 64)
 #undef DW3
         throw std::runtime_error("gemm3: unknown dense WGRAD variant " + std::to_string(variant));
@@ -2783,8 +2783,36 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef NW
         else throw std::runtime_error("gemm3: unknown narrow WGRAD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
-        return;
+        return true;
     }
+    if (mode == MODE_WGRAD && variant < 3000000) {     // (3000000 .. 3999999: conv WGRAD, part 1)
+        const bool gen = variant >= 1000000;
+        const int v = variant % 1000000;
+        // v = BMF * 1000 + BNK (+ 500: two row groups per block, 512 threads)
+#define W3(BMF_, BNK_) \
+    if (v == BMF_ * 1000 + BNK_) { \
+        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return true; } \
+    if (v == BMF_ * 1000 + BNK_ + 500) { \
+        const dim3 b2(512); \
+        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true, 4, 2>), grid, b2, 0, s, dp, tp); \
+        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 4, 2>), grid, b2, 0, s, dp, tp); \
+        SERANN_CHECK(hipGetLastError()); return true; }
+        W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
+        // whole-F tiles of single-split Dense WGRADs (hip_ops.WGRAD_WIDE): X read once per column tile
+        W3(96, 64) W3(128, 64) W3(160, 64) W3(192, 64)
+#undef W3
+        throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
+    }
+    return false;
+}
+#endif
+
+#if G3_PART(1)
+// part 1: LDS-halo conv WGRAD
+bool gemm3_launch_part1(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
+                          const int4* tp) {
     if (mode == MODE_WGRAD && variant >= 3000000) {
         const int tier = (variant / 100000) % 10;
         const int v = variant % 100000;
@@ -2792,7 +2820,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     if (v == BMF_ * 1000 + BNK_ / 64 && tier == TIER_) {                                                   \
         hipLaunchKernelGGL((g3_conv_wgrad_kernel<BMF_, BNK_, PATCH_>), grid, block, 0, s, dp, tp);     \
         SERANN_CHECK(hipGetLastError());                                                              \
-        return;                                                                                       \
+        return true;                                                                                       \
     }
 #define CW3(BMF_, BNK_) CW3T(BMF_, BNK_, 0, 8192) CW3T(BMF_, BNK_, 1, 16384) CW3T(BMF_, BNK_, 2, 32768)
         // (the 64 KB patch tier is instantiated for 16-filter blocks only: two stages of it fill the LDS)
@@ -2804,33 +2832,21 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef CW3
         throw std::runtime_error("gemm3: unknown conv WGRAD variant " + std::to_string(variant));
     }
-    if (mode == MODE_WGRAD) {
-        const bool gen = variant >= 1000000;
-        const int v = variant % 1000000;
-        // v = BMF * 1000 + BNK (+ 500: two row groups per block, 512 threads)
-#define W3(BMF_, BNK_) \
-    if (v == BMF_ * 1000 + BNK_) { \
-        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true>), grid, block, 0, s, dp, tp); \
-        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false>), grid, block, 0, s, dp, tp); \
-        SERANN_CHECK(hipGetLastError()); return; } \
-    if (v == BMF_ * 1000 + BNK_ + 500) { \
-        const dim3 b2(512); \
-        if (gen) hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, true, 4, 2>), grid, b2, 0, s, dp, tp); \
-        else hipLaunchKernelGGL((g3_wgrad_kernel<BMF_, BNK_, false, 4, 2>), grid, b2, 0, s, dp, tp); \
-        SERANN_CHECK(hipGetLastError()); return; }
-        W3(64, 128) W3(64, 64) W3(32, 128) W3(32, 64) W3(16, 256) W3(16, 128) W3(16, 64) W3(64, 16)
-        // whole-F tiles of single-split Dense WGRADs (hip_ops.WGRAD_WIDE): X read once per column tile
-        W3(96, 64) W3(128, 64) W3(160, 64) W3(192, 64)
-#undef W3
-        throw std::runtime_error("gemm3: unknown WGRAD variant " + std::to_string(variant));
-    }
+    return false;
+}
+#endif
+
+#if G3_PART(2)
+// part 2: conv FWD and LDS-tiled FWD / DGRAD
+bool gemm3_launch_part2(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
+                          const int4* tp) {
     if (mode == MODE_FWD && variant >= 2000 && variant < 3000) {
         const int v = variant - 2000;
 #define C3T(NT_, RT_, TIER_, PATCH_)                                                                  \
     if (v == 100 * TIER_ + NT_ + 10 * RT_) {                                                          \
         hipLaunchKernelGGL((g3_conv_fwd_kernel<NT_, RT_, PATCH_>), grid, block, 0, s, dp, tp);         \
         SERANN_CHECK(hipGetLastError());                                                              \
-        return;                                                                                       \
+        return true;                                                                                       \
     }
 #define C3(NT_, RT_) C3T(NT_, RT_, 0, 8192) C3T(NT_, RT_, 1, 16384) C3T(NT_, RT_, 2, 32768)
         C3(1, 1) C3(2, 1) C3(4, 1) C3(1, 2) C3(2, 2) C3(4, 2) C3(1, 4) C3(2, 4) C3(4, 4)
@@ -2847,7 +2863,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         TL(64) TL(128) TL(160) TL(192)
 #undef TL
         SERANN_CHECK(hipGetLastError());
-        return;
+        return true;
     }
     if (mode == MODE_DGRAD && variant > 17000 && variant < 19000) {
         // GF_NBNSUM: the BN-backward-sums epilogue (17000 + BN: transposed weights, 18000 + BN: natural)
@@ -2858,7 +2874,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef TLS
         throw std::runtime_error("gemm3: unknown NBNSUM DGRAD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
-        return;
+        return true;
     }
     if (mode == MODE_DGRAD && (variant == 8064 || variant == 8128 || variant == 8160 || variant == 8192)) {
         // BT: natural-layout weights
@@ -2867,8 +2883,16 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
         else if (variant == 8160) hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 160, true>), grid, block, 0, s, dp, tp);
         else hipLaunchKernelGGL((g3_tiled_kernel<MODE_DGRAD, 192, true>), grid, block, 0, s, dp, tp);
         SERANN_CHECK(hipGetLastError());
-        return;
+        return true;
     }
+    return false;
+}
+#endif
+
+#if G3_PART(3)
+// part 3: narrow FWD, single-step and direct-fragment FWD / DGRAD
+bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
+                          const int4* tp) {
     if (mode == MODE_FWD && variant >= 6000 && variant < 7000) {
         const int k = (variant - 6000) % 100;
         const bool st = (variant - 6000) >= 100, sr = (variant - 6000) >= 200;
@@ -2879,7 +2903,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
 #undef NF
         else throw std::runtime_error("gemm3: unknown narrow FWD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
-        return;
+        return true;
     }
     if (variant >= 5000) {
         const int v = variant - 5000;
@@ -2887,7 +2911,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     if (mode == MODE_ && v == NT_ + 10 * RT_) {                                                         \
         hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, false, false, true>), grid, block, 0, s, dp, tp); \
         SERANN_CHECK(hipGetLastError());                                                                \
-        return;                                                                                         \
+        return true;                                                                                         \
     }
         S3(MODE_FWD, 1, 4) S3(MODE_FWD, 2, 4) S3(MODE_FWD, 4, 4) S3(MODE_FWD, 8, 2)
         S3(MODE_DGRAD, 1, 4) S3(MODE_DGRAD, 2, 4) S3(MODE_DGRAD, 4, 4) S3(MODE_DGRAD, 8, 2)
@@ -2902,7 +2926,7 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     if (mode == MODE_ && nt == NT_ && rt == RT_ && kw == KW_) { \
         if (gen) hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, KW_, true>), grid, block, 0, s, dp, tp); \
         else hipLaunchKernelGGL((g3_direct_kernel<MODE_, NT_, RT_, KW_, false>), grid, block, 0, s, dp, tp); \
-        SERANN_CHECK(hipGetLastError()); return; }
+        SERANN_CHECK(hipGetLastError()); return true; }
 #define D3ALL(MODE_) \
     D3(MODE_, 1, 4, false) D3(MODE_, 2, 4, false) D3(MODE_, 4, 4, false) \
     D3(MODE_, 1, 2, false) D3(MODE_, 2, 2, false) D3(MODE_, 4, 2, false) D3(MODE_, 8, 2, false) \
@@ -2911,5 +2935,20 @@ void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t
     D3ALL(MODE_DGRAD)
 #undef D3ALL
 #undef D3
+    return false;
+}
+#endif
+
+#if G3_PART(0)
+void launch_gemm3(int mode, int variant, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
+    if (ntiles <= 0) return;
+    hipStream_t s = as_stream(stream);
+    const GemmDesc* dp = as_ptr<const GemmDesc>(descs);
+    const int4* tp = as_ptr<const int4>(tiles);
+    dim3 grid((unsigned)ntiles), block(256);
+    if (gemm3_launch_part0(mode, variant, grid, block, s, dp, tp) || gemm3_launch_part1(mode, variant, grid, block, s, dp, tp) ||
+        gemm3_launch_part2(mode, variant, grid, block, s, dp, tp) || gemm3_launch_part3(mode, variant, grid, block, s, dp, tp))
+        return;
     throw std::runtime_error("gemm3: unknown variant " + std::to_string(variant));
 }
+#endif

@@ -63,8 +63,14 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("splitk_finalize", &launch_splitk_finalize);
     m.def("wgrad_finalize", &launch_wgrad_finalize);
     m.def("rep_bits", &launch_rep_bits);
-    m.def("concrete_fwd", &launch_concrete_fwd);
-    m.def("concrete_bwd", &launch_concrete_bwd);
-    m.def("cat_loglik_fwd", &launch_cat_loglik_fwd);
-    m.def("cat_loglik_bwd", &launch_cat_loglik_bwd);
+    m.def("concrete_fwd", &launch_concrete_fwd, py::arg("logits"), py::arg("u"), py::arg("s"), py::arg("z"), py::arg("kl"),
+          py::arg("B"), py::arg("G"), py::arg("A"), py::arg("t"), py::arg("tp"), py::arg("seed"), py::arg("offset"),
+          py::arg("stream"), py::arg("zb") = 0);
+    m.def("concrete_bwd", &launch_concrete_bwd, py::arg("s"), py::arg("z"), py::arg("gz"), py::arg("gkl"), py::arg("dlogits"),
+          py::arg("B"), py::arg("G"), py::arg("A"), py::arg("t"), py::arg("tp"), py::arg("stream"), py::arg("bf16") = 0);
+    m.def("cat_loglik_fwd", &launch_cat_loglik_fwd, py::arg("z"), py::arg("x"), py::arg("out"), py::arg("B"), py::arg("L"),
+          py::arg("V"), py::arg("stream"), py::arg("bf16") = 0);
+    m.def("cat_loglik_bwd", &launch_cat_loglik_bwd, py::arg("z"), py::arg("x"), py::arg("gout"), py::arg("dz"), py::arg("B"),
+          py::arg("L"), py::arg("V"), py::arg("stream"), py::arg("bf16") = 0);
+    m.def("onehot", &launch_onehot);
 }

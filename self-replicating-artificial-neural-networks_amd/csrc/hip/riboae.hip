@@ -32,41 +32,62 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
     return threadIdx.x == 0 ? ((red[0] + red[1]) + red[2]) + red[3] : 0.f;
 }
 
-__global__ __launch_bounds__(256) void cat_loglik_fwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ x,
+// Element access of the K37 kernels: z fp32 or bf16 (the generative BatchNormalization's own output, read in place
+// by the HIP trainer), targets int64 or int32, dz fp32 or bf16 (the bf16 gradient buffer the next BN backward reads)
+template <typename T> __device__ __forceinline__ float ld_f(const T* p, int64_t i);
+template <> __device__ __forceinline__ float ld_f<float>(const float* p, int64_t i) { return p[i]; }
+template <> __device__ __forceinline__ float ld_f<bf16_t>(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ void st_f(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st_f(bf16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
+
+template <typename ZT, typename XT>
+__global__ __launch_bounds__(256) void cat_loglik_fwd_kernel(const ZT* __restrict__ z, const XT* __restrict__ x,
                                                              float* __restrict__ out, int B, int L, int V) {
     __shared__ float red[4];
     const int b = blockIdx.x;
     float v = 0.f;
     for (int l = threadIdx.x; l < L; l += 256) {
-        const float* row = z + ((int64_t)b * L + l) * V;
+        const int64_t row = ((int64_t)b * L + l) * V;
         float m = -INFINITY;
-        for (int k = 0; k < V; ++k) m = fmaxf(m, row[k]);
+        for (int k = 0; k < V; ++k) m = fmaxf(m, ld_f(z, row + k));
         float s = 0.f;
-        for (int k = 0; k < V; ++k) s += __expf(row[k] - m);
+        for (int k = 0; k < V; ++k) s += __expf(ld_f(z, row + k) - m);
         int t = (int)x[(int64_t)b * L + l];
         t = min(max(t, 0), V - 1);
-        v += row[t] - m - __logf(s);
+        v += ld_f(z, row + t) - m - __logf(s);
     }
     v = block_sum256(v, red);
     if (threadIdx.x == 0) out[b] = v;
 }
 
-__global__ __launch_bounds__(256) void cat_loglik_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ x,
-                                                             const float* __restrict__ gout, float* __restrict__ dz,
+template <typename ZT, typename XT, typename DT>
+__global__ __launch_bounds__(256) void cat_loglik_bwd_kernel(const ZT* __restrict__ z, const XT* __restrict__ x,
+                                                             const float* __restrict__ gout, DT* __restrict__ dz,
                                                              int B, int L, int V) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (int64_t)B * L) return;
     const int b = (int)(gid / L);
-    const float* row = z + gid * V;
-    float* drow = dz + gid * V;
+    const int64_t row = gid * V;
     float m = -INFINITY;
-    for (int k = 0; k < V; ++k) m = fmaxf(m, row[k]);
+    for (int k = 0; k < V; ++k) m = fmaxf(m, ld_f(z, row + k));
     float s = 0.f;
-    for (int k = 0; k < V; ++k) s += __expf(row[k] - m);
+    for (int k = 0; k < V; ++k) s += __expf(ld_f(z, row + k) - m);
     const float inv = 1.f / s, g = gout[b];
     int t = (int)x[gid];
     t = min(max(t, 0), V - 1);
-    for (int k = 0; k < V; ++k) drow[k] = g * ((k == t ? 1.f : 0.f) - __expf(row[k] - m) * inv);
+    for (int k = 0; k < V; ++k) st_f(dz, row + k, g * ((k == t ? 1.f : 0.f) - __expf(ld_f(z, row + k) - m) * inv));
+}
+
+// One-hot rows of the target tokens (the embedding WGRAD's A operand), bf16 [rows][V]: written by a kernel from the
+// int32 tokens instead of a host-side int64 one_hot + cast (57 MB of int64 per RiboAE step at B = 512)
+__global__ __launch_bounds__(256) void onehot_kernel(const int* __restrict__ tok, bf16_t* __restrict__ out, int64_t rows,
+                                                     int V) {
+    const int64_t total = rows * V;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / V;
+        const int v = (int)(i - r * V);
+        out[i] = v == min(max(tok[r], 0), V - 1) ? (bf16_t)0x3f80 : (bf16_t)0;
+    }
 }
 
 // ---- K36 -------------------------------------------------------------------------------------------
@@ -88,6 +109,7 @@ constexpr int CONCRETE_MAX_A = 16;
 
 __global__ __launch_bounds__(256) void concrete_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ u_in,
                                                            float* __restrict__ s_out, float* __restrict__ z_out,
+                                                           bf16_t* __restrict__ zb_out,
                                                            float* __restrict__ kl, int B, int G, int A, float t, float tp,
                                                            uint32_t k0, uint32_t k1, uint32_t off) {
     __shared__ float red[4];
@@ -126,16 +148,19 @@ __global__ __launch_bounds__(256) void concrete_fwd_kernel(const float* __restri
         const float inv = 1.f / den;
         for (int a = 0; a < A; ++a) {
             s_out[row * A + a] = s[a];
-            z_out[row * A + a] = expf(s[a] - m) * inv;
+            const float za = expf(s[a] - m) * inv;
+            z_out[row * A + a] = za;
+            if (zb_out) zb_out[row * A + a] = f2bf(za);     // the decoder's bf16 input
         }
     }
     klv = block_sum256(klv, red);
     if (threadIdx.x == 0) kl[b] = klv;           // fixed-order block sum: no atomics (deterministic)
 }
 
+template <typename GT, typename DT>
 __global__ __launch_bounds__(256) void concrete_bwd_kernel(const float* __restrict__ s_in, const float* __restrict__ z_in,
-                                                           const float* __restrict__ gz, const float* __restrict__ gkl,
-                                                           float* __restrict__ dlogits, int B, int G, int A, float t,
+                                                           const GT* __restrict__ gz, const float* __restrict__ gkl,
+                                                           DT* __restrict__ dlogits, int B, int G, int A, float t,
                                                            float tp) {
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= (int64_t)B * G) return;
@@ -144,48 +169,76 @@ __global__ __launch_bounds__(256) void concrete_bwd_kernel(const float* __restri
     const float gk = gkl ? gkl[b] : 0.f;
     float dot = 0.f;
     if (gz)
-        for (int a = 0; a < A; ++a) dot += z_in[row * A + a] * gz[row * A + a];
+        for (int a = 0; a < A; ++a) dot += z_in[row * A + a] * ld_f(gz, row * A + a);
     for (int a = 0; a < A; ++a) {
         const float za = z_in[row * A + a];
-        const float ds = gz ? za * (gz[row * A + a] - dot) : 0.f;
+        const float ds = gz ? za * (ld_f(gz, row * A + a) - dot) : 0.f;
         const float zp = (s_in[row * A + a] - ploc) * tp;
-        dlogits[row * A + a] = inv_t * (ds + gk * tp * (1.f - expf(-zp)));
+        st_f(dlogits, row * A + a, inv_t * (ds + gk * tp * (1.f - expf(-zp))));
     }
 }
 
 void launch_concrete_fwd(uint64_t logits, uint64_t u, uint64_t s, uint64_t z, uint64_t kl, int64_t B, int64_t G,
-                         int64_t A, double t, double tp, uint64_t seed, uint64_t offset, uint64_t stream) {
+                         int64_t A, double t, double tp, uint64_t seed, uint64_t offset, uint64_t stream, uint64_t zb) {
     if (B <= 0 || G <= 0) return;
     if (A < 1 || A > CONCRETE_MAX_A) throw std::runtime_error("concrete: alphabet size must be in [1, 16]");
     hipLaunchKernelGGL(concrete_fwd_kernel, dim3((unsigned)B), dim3(256), 0, as_stream(stream),
                        as_ptr<const float>(logits), as_ptr<const float>(u), as_ptr<float>(s), as_ptr<float>(z),
-                       as_ptr<float>(kl), (int)B, (int)G, (int)A, (float)t, (float)tp, (uint32_t)seed,
+                       as_ptr<bf16_t>(zb), as_ptr<float>(kl), (int)B, (int)G, (int)A, (float)t, (float)tp, (uint32_t)seed,
                        (uint32_t)(seed >> 32), (uint32_t)offset);
     SERANN_CHECK(hipGetLastError());
 }
 
+// bf16: 1 = gz is bf16 and dlogits is written as bf16 (the HIP trainer's buffers), 0 = both fp32
 void launch_concrete_bwd(uint64_t s, uint64_t z, uint64_t gz, uint64_t gkl, uint64_t dlogits, int64_t B, int64_t G,
-                         int64_t A, double t, double tp, uint64_t stream) {
+                         int64_t A, double t, double tp, uint64_t stream, int bf16) {
     if (B <= 0 || G <= 0) return;
-    hipLaunchKernelGGL(concrete_bwd_kernel, dim3((unsigned)((B * G + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       as_ptr<const float>(s), as_ptr<const float>(z), as_ptr<const float>(gz),
-                       as_ptr<const float>(gkl), as_ptr<float>(dlogits), (int)B, (int)G, (int)A, (float)t, (float)tp);
+    const dim3 grid((unsigned)((B * G + 255) / 256));
+    if (bf16)
+        hipLaunchKernelGGL((concrete_bwd_kernel<bf16_t, bf16_t>), grid, dim3(256), 0, as_stream(stream),
+                           as_ptr<const float>(s), as_ptr<const float>(z), as_ptr<const bf16_t>(gz),
+                           as_ptr<const float>(gkl), as_ptr<bf16_t>(dlogits), (int)B, (int)G, (int)A, (float)t, (float)tp);
+    else
+        hipLaunchKernelGGL((concrete_bwd_kernel<float, float>), grid, dim3(256), 0, as_stream(stream),
+                           as_ptr<const float>(s), as_ptr<const float>(z), as_ptr<const float>(gz),
+                           as_ptr<const float>(gkl), as_ptr<float>(dlogits), (int)B, (int)G, (int)A, (float)t, (float)tp);
     SERANN_CHECK(hipGetLastError());
 }
 
 // ---- K37 -------------------------------------------------------------------------------------------
-void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream) {
+// bf16: 1 = z bf16, x int32, dz bf16 (the HIP trainer); 0 = z fp32, x int64, dz fp32 (riboae_ops autograd)
+void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream,
+                           int bf16) {
     if (B <= 0 || L <= 0) return;
-    hipLaunchKernelGGL(cat_loglik_fwd_kernel, dim3((unsigned)B), dim3(256), 0, as_stream(stream),
-                       as_ptr<const float>(z), as_ptr<const int64_t>(x), as_ptr<float>(out), (int)B, (int)L, (int)V);
+    if (bf16)
+        hipLaunchKernelGGL((cat_loglik_fwd_kernel<bf16_t, int>), dim3((unsigned)B), dim3(256), 0, as_stream(stream),
+                           as_ptr<const bf16_t>(z), as_ptr<const int>(x), as_ptr<float>(out), (int)B, (int)L, (int)V);
+    else
+        hipLaunchKernelGGL((cat_loglik_fwd_kernel<float, int64_t>), dim3((unsigned)B), dim3(256), 0, as_stream(stream),
+                           as_ptr<const float>(z), as_ptr<const int64_t>(x), as_ptr<float>(out), (int)B, (int)L, (int)V);
     SERANN_CHECK(hipGetLastError());
 }
 
 void launch_cat_loglik_bwd(uint64_t z, uint64_t x, uint64_t gout, uint64_t dz, int64_t B, int64_t L, int64_t V,
-                           uint64_t stream) {
+                           uint64_t stream, int bf16) {
     if (B <= 0 || L <= 0) return;
-    hipLaunchKernelGGL(cat_loglik_bwd_kernel, dim3((unsigned)((B * L + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       as_ptr<const float>(z), as_ptr<const int64_t>(x), as_ptr<const float>(gout), as_ptr<float>(dz),
-                       (int)B, (int)L, (int)V);
+    const dim3 grid((unsigned)((B * L + 255) / 256));
+    if (bf16)
+        hipLaunchKernelGGL((cat_loglik_bwd_kernel<bf16_t, int, bf16_t>), grid, dim3(256), 0, as_stream(stream),
+                           as_ptr<const bf16_t>(z), as_ptr<const int>(x), as_ptr<const float>(gout), as_ptr<bf16_t>(dz),
+                           (int)B, (int)L, (int)V);
+    else
+        hipLaunchKernelGGL((cat_loglik_bwd_kernel<float, int64_t, float>), grid, dim3(256), 0, as_stream(stream),
+                           as_ptr<const float>(z), as_ptr<const int64_t>(x), as_ptr<const float>(gout), as_ptr<float>(dz),
+                           (int)B, (int)L, (int)V);
+    SERANN_CHECK(hipGetLastError());
+}
+
+void launch_onehot(uint64_t tok, uint64_t out, int64_t rows, int64_t V, uint64_t stream) {
+    if (rows <= 0) return;
+    int64_t blocks = (rows * V + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(onehot_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), as_ptr<const int>(tok),
+                       as_ptr<bf16_t>(out), rows, (int)V);
     SERANN_CHECK(hipGetLastError());
 }

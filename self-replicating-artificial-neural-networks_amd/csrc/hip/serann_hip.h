@@ -46,6 +46,11 @@ enum GemmFlags : int64_t {
                           // (its only consumer recomputes it: nbn.hip)
     GF_BNUSTAT = 1024,    // FWD (conv-halo, direct non-KW, LDS-tiled without k splits): also accumulate the consuming
                           // BatchNorm's phase-0 statistics, unshifted, into aux (its workspace; BnDesc flag 512)
+    GF_WSLAB = 2048,      // WGRAD (Dense / 1x1 kernels), m-split problem: a block stores its fp32 partial tile to the
+                          // slab of its split, ext + (kt0 / kper) * M * N (plain stores, every element written once
+                          // per split); wgrad_finalize sums the S slabs in split order (WgFinDesc with C = Cp = N) and
+                          // stores the Q40 gradient or applies Adam -- no fixed-point atomics, so the reduction can
+                          // be split as finely as the grid needs
     GF_NBNSUM = 512,      // DGRAD (LDS-tiled kernel) producing the output gradient of a fused raw-input
                           // Dense (1 input channel) -> BN pair (ext = its NbnDesc): instead of storing dY, reduce the BN / Dense
                           // backward sums of every column over the block's rows into NbnDesc::part; nbn
@@ -74,12 +79,14 @@ void launch_loss(int train, uint64_t descs, int64_t nprob, int64_t B, uint64_t s
 void launch_memset32(uint64_t ptr, int64_t n, uint64_t stream);
 void launch_imcol(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 void launch_concrete_fwd(uint64_t logits, uint64_t u, uint64_t s, uint64_t z, uint64_t kl, int64_t B, int64_t G,
-                         int64_t A, double t, double tp, uint64_t seed, uint64_t offset, uint64_t stream);
+                         int64_t A, double t, double tp, uint64_t seed, uint64_t offset, uint64_t stream, uint64_t zb);
 void launch_concrete_bwd(uint64_t s, uint64_t z, uint64_t gz, uint64_t gkl, uint64_t dlogits, int64_t B, int64_t G,
-                         int64_t A, double t, double tp, uint64_t stream);
-void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream);
+                         int64_t A, double t, double tp, uint64_t stream, int bf16);
+void launch_cat_loglik_fwd(uint64_t z, uint64_t x, uint64_t out, int64_t B, int64_t L, int64_t V, uint64_t stream,
+                           int bf16);
 void launch_cat_loglik_bwd(uint64_t z, uint64_t x, uint64_t gout, uint64_t dz, int64_t B, int64_t L, int64_t V,
-                           uint64_t stream);
+                           uint64_t stream, int bf16);
+void launch_onehot(uint64_t tok, uint64_t out, int64_t rows, int64_t V, uint64_t stream);
 void launch_splitk_finalize(uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 // Split WGRAD finalize (aux.hip): a WGRAD problem split over S row ranges leaves one fp32 slab per split,
 // ws[S][M][ldp] with ldp = (N / C) * Cp (the kernel's padded (tap, Cp) columns; Cp = C for Dense), written

@@ -166,6 +166,10 @@ def _al(n: int) -> int:
     return (int(n) + ALIGN - 1) // ALIGN * ALIGN
 
 
+# split WGRADs' ordered finalize applies Adam to the weights it writes (SERANN_FINALIZE_ADAM=0: the arena pass does)
+FINALIZE_ADAM = os.environ.get("SERANN_FINALIZE_ADAM", "1") != "0"
+
+
 class Arena:
     """Bump allocator over one device tensor."""
 
@@ -431,9 +435,8 @@ class HipPopulationEngine(PopulationEngine):
         self.mom_mode = H.MOM_16 if self.cfg.adam_moments == "16bit" else H.MOM_F32
         m16 = self.mom_mode == H.MOM_16
         self.m = torch.zeros(self.p.numel(), dtype=torch.bfloat16 if m16 else torch.float32, device=dev)
-        # (log16 v: int16 code -32768 is v = 0)
-        self.v = (torch.full((self.p.numel(),), -32768, dtype=torch.int16, device=dev) if m16
-                  else torch.zeros(self.p.numel(), dtype=torch.float32, device=dev))
+        # (log16 v: 16-bit codes held in int16, code 0 is v = 0)
+        self.v = torch.zeros(self.p.numel(), dtype=torch.int16 if m16 else torch.float32, device=dev)
         self.pbf = torch.zeros(self.p.numel() + SLACK, dtype=torch.bfloat16, device=dev)
         self.stats = self.sarena.materialize()
         self.step_i = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -776,12 +779,18 @@ class HipPopulationEngine(PopulationEngine):
                                         S=ns, act=r.get("act", 0)))
                 # split conv WGRADs: fp32 slabs per split (every element written), summed in split order by
                 # one grouped wgrad_finalize launch after the GEMM (no fixed-point atomics)
+                # (conv WGRADs' padded slabs, Dense / 1x1 m-splits' [M][N] slabs: GF_WSLAB); the finalize is the
+                # sole writer of those weights, so it applies Adam too when the plan fuses the optimizer
                 wfin = []
                 for r in rws:
                     if r.get("_wgfin"):
                         wsw = torch.empty(H.wgrad_slab_elems(r) + SLACK, dtype=torch.float32, device=self.device)
                         plan.keep.append(wsw)
-                        wfin.append(H.wgrad_finalize_row(r, wsw.data_ptr()))
+                        fadam = int(r.get("adam") or 0) if FINALIZE_ADAM else 0
+                        wfin.append(H.wgrad_finalize_row(r, wsw.data_ptr(), fadam))
+                        if fadam:
+                            plan.adam_regions.append(((int(r["out"]) - self.g.data_ptr()) // 8, int(r["M"]),
+                                                      int(r["N"]), int(r.get("ldo") or r["N"])))
                 plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
                                             len(tiles)))
                 if wfin:

@@ -58,6 +58,7 @@ BN_USTAT = 512
 GF_NBNSUM = 512
 GF_NOSTORE = 32
 GF_ADAM = 256
+GF_WSLAB = 2048        # Dense / 1x1 WGRAD m-split: fp32 slab per split + ordered wgrad_finalize (serann_hip.h)
 ADAM_CTX_DTYPE = np.dtype([(f, _I) for f in ['p', 'm', 'v', 'pbf', 'g', 'lr_t', 'org_off', 'diverged', 'norg']]
                           + [(f, np.float32) for f in ['b1', 'b2', 'eps']]
                           + [("mode", np.int32)])
@@ -198,11 +199,12 @@ def from_qg(t):
 
 def moments_f32(m, v) -> tuple:
     """The Adam moment arenas as fp32 tensors, whatever their storage (csrc/hip/common.h MOM_*): fp32 as is,
-    bf16 m widened, log16 v (int16 q: v = 2^(q / 1024), q = -32768: 0) decoded."""
+    bf16 m widened, log16 v (16-bit code q held in int16: v = 2^(q / 819.2 - 48), q = 0: 0) decoded."""
     import torch
     if v.dtype == torch.int16:
-        vf = torch.exp2(v.float() / 1024.0)
-        vf = torch.where(v == -32768, torch.zeros_like(vf), vf)
+        q = v.to(torch.int32) & 0xffff
+        vf = torch.exp2(q.double() / 819.2 - 48.0).float()
+        vf = torch.where(q == 0, torch.zeros_like(vf), vf)
         return m.float(), vf
     return m.float(), v.float()
 
@@ -870,10 +872,19 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 for (r, (M, N, K)), t_ in zip(items, tg):
-                    if wgrad_splits(K, t_, min(32, t_)) == 1:
+                    ns = wgrad_splits(K, t_, min(32, t_))
+                    if ns == 1:
                         r["flags"] = int(r.get("flags", 0)) | GF_WSTORE
                         if r.get("adam"):
                             r["flags"] |= GF_ADAM      # sole writer: apply the optimizer step in the epilogue
+                    elif WGRAD_SLABS:
+                        # m-split: fp32 slab per split, summed in split order by wgrad_finalize (which also applies
+                        # Adam when the row carries an AdamCtx); the caller allocates the slabs (ext)
+                        kt = -(-K // BK)
+                        r["kper"] = -(-kt // ns)
+                        r["_wgfin"] = -(-kt // r["kper"])
+                        r["_ldp"] = N
+                        r["flags"] = int(r.get("flags", 0)) | GF_WSLAB
                     else:
                         r["adam"] = 0
             elif mode == MODE_FWD and 7000 < v < 7300:
@@ -936,12 +947,17 @@ def dwgrad_ok(geo: dict, M: int, N: int, v: int) -> bool:
 
 
 def wgrad_finalize_row(r: dict, ws_ptr: int, adam: int = 0) -> dict:
-    """WgFinDesc of a split conv WGRAD row (``_wgfin`` set by gemm3_plan) whose slabs live at ``ws_ptr``
-    (``wgrad_slab_elems(r)`` fp32); sets the row's ``ext``."""
+    """WgFinDesc of a split WGRAD row (``_wgfin`` set by gemm3_plan: a conv WGRAD's padded (tap, Cp) slabs, or a
+    Dense / 1x1 WGRAD's [M][N] slabs, GF_WSLAB) whose slabs live at ``ws_ptr`` (``wgrad_slab_elems(r)`` fp32); sets
+    the row's ``ext``.  ``adam``: device AdamCtx -- the finalize applies the optimizer step (sole writer)."""
     r["ext"] = ws_ptr
-    C = int(r["C"])
-    return dict(ws=ws_ptr, out=int(r["out"]), adam=adam, M=int(r["M"]), N=int(r["N"]), C=C, Cp=-(-C // 8) * 8,
-                S=int(r["_wgfin"]), flags=0)
+    if int(r.get("flags", 0)) & GF_WSLAB:
+        C = Cp = int(r["N"])                     # one "tap" of N columns, unpadded
+    else:
+        C = int(r["C"])
+        Cp = -(-C // 8) * 8
+    return dict(ws=ws_ptr, out=int(r["out"]), adam=adam, M=int(r["M"]), N=int(r["N"]), C=C, Cp=Cp,
+                S=int(r["_wgfin"]), ldo=int(r.get("ldo", 0) or 0), flags=0)
 
 
 def wgrad_slab_elems(r: dict) -> int:
@@ -1030,6 +1046,8 @@ DWGRAD = _os.environ.get("SERANN_DWGRAD", "0") != "0"
 DWGRAD_RG = int(_os.environ.get("SERANN_DWGRAD_RG", "2"))
 DWGRAD_CALIGN = int(_os.environ.get("SERANN_DWGRAD_CALIGN", "8"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
+# Dense / 1x1 WGRAD m-splits meet in fp32 slabs + an ordered finalize (GF_WSLAB, round 6) instead of Q40 atomics
+WGRAD_SLABS = _os.environ.get("SERANN_WGRAD_SLABS", "1") != "0"
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 

@@ -198,8 +198,10 @@ class HipRiboTrainer:
             buf["d" + k] = _zeros(n, bf, dev)              # gradient wrt the BN output
             buf["dz" + k] = _zeros(n, bf, dev)             # gradient wrt the layer output (BN dx)
         self.shapes = shapes
+        # (the kernels read and write the dtypes their neighbours use: int32 tokens, a bf16 one-hot from a kernel,
+        # bf16 z / dz / dlogits and the generative BN's bf16 output read in place by the log-likelihood kernels --
+        # no dtype-shuttling copies in the step)
         buf["tok"] = torch.zeros(B * L + SLACK, dtype=torch.int32, device=dev)
-        buf["tok64"] = torch.zeros(B * L, dtype=torch.int64, device=dev)
         buf["onehot"] = _zeros(B * L * V, bf, dev)
         buf["logits"] = _zeros(B * G * A, torch.float32, dev)
         buf["s"] = _zeros(B * G * A, torch.float32, dev)
@@ -207,8 +209,6 @@ class HipRiboTrainer:
         buf["kl"] = _zeros(B, torch.float32, dev)
         buf["zb"] = _zeros(B * G * A, bf, dev)
         buf["dzb"] = _zeros(B * G * A, bf, dev)
-        buf["dzf"] = _zeros(B * G * A, torch.float32, dev)
-        buf["dlogits"] = _zeros(B * G * A, torch.float32, dev)
         buf["dlogitsb"] = _zeros(B * G * A, bf, dev)
         n1 = B * self.gflat
         for k in ("h1", "yh1", "dh1", "dzh1"):
@@ -216,8 +216,6 @@ class HipRiboTrainer:
         n2 = B * L * V
         for k in ("h2", "yh2", "dh2", "dzh2"):
             buf[k] = _zeros(n2, bf, dev)
-        buf["yh2f"] = _zeros(n2, torch.float32, dev)
-        buf["dyh2f"] = _zeros(n2, torch.float32, dev)
         buf["logpx"] = _zeros(B, torch.float32, dev)
         buf["gout"] = _zeros(B, torch.float32, dev)
         buf["gkl"] = _zeros(B, torch.float32, dev)
@@ -463,11 +461,8 @@ class HipRiboTrainer:
             # step counter and lr_t first: the fused-Adam WGRAD epilogues read lr_t during the backward
             lib.adam_scalars(self.step_i.data_ptr(), self.lr_t.data_ptr(), float(lr), self.b1, self.b2, s)
         buf = pl.buf
-        tok = tokens.to(self.dev)
-        buf["tok"][:B * L].copy_(tok.reshape(-1))
-        buf["tok64"].copy_(tok.reshape(-1))
-        buf["onehot"][:B * L * V].view(B * L, V).copy_(
-            torch.nn.functional.one_hot(buf["tok64"], V).to(torch.bfloat16))
+        buf["tok"][:B * L].copy_(tokens.reshape(-1))      # (device-resident int32 batches: a device copy)
+        lib.onehot(buf["tok"].data_ptr(), buf["onehot"].data_ptr(), B * L, V, s)
         lib.memset32(buf["ws"].data_ptr(), 2 * buf["ws"].numel(), s)
         lib.transpose_weights(pl.trans[0].data_ptr(), pl.trans[1].data_ptr(), len(pl.trans[1]), s)
         lib.embed_gather(buf["tok"].data_ptr(), self.bptr("emb"), buf["e0"].data_ptr(), B * L, E, V, s)
@@ -481,26 +476,19 @@ class HipRiboTrainer:
             noise = noise.to(self.dev, torch.float32).contiguous()
             uptr, seed, off = noise.data_ptr(), 0, 0
         lib.concrete_fwd(buf["logits"].data_ptr(), uptr, buf["s"].data_ptr(), buf["z"].data_ptr(), buf["kl"].data_ptr(),
-                         B, G, A, float(temperature), tp, int(seed), off, s)
-        buf["zb"][:B * G * A].copy_(buf["z"][:B * G * A])
+                         B, G, A, float(temperature), tp, int(seed), off, s, buf["zb"].data_ptr())
         self._run(pl.fwd_dec)
-        n2 = B * L * V
-        buf["yh2f"][:n2].copy_(buf["yh2"][:n2])
-        lib.cat_loglik_fwd(buf["yh2f"].data_ptr(), buf["tok64"].data_ptr(), buf["logpx"].data_ptr(), B, L, V, s)
+        lib.cat_loglik_fwd(buf["yh2"].data_ptr(), buf["tok"].data_ptr(), buf["logpx"].data_ptr(), B, L, V, s, 1)
         logpx, kl = buf["logpx"][:B], buf["kl"][:B]
         nelbo = -(logpx - kld_weight * kl).mean()
         # backward: d nelbo / d logpx = -1/B, d / d kl = w/B
         buf["gout"][:B].fill_(-1.0 / B)
         buf["gkl"][:B].fill_(float(kld_weight) / B)
-        lib.cat_loglik_bwd(buf["yh2f"].data_ptr(), buf["tok64"].data_ptr(), buf["gout"].data_ptr(),
-                           buf["dyh2f"].data_ptr(), B, L, V, s)
-        buf["dh2"][:n2].copy_(buf["dyh2f"][:n2])
+        lib.cat_loglik_bwd(buf["yh2"].data_ptr(), buf["tok"].data_ptr(), buf["gout"].data_ptr(),
+                           buf["dh2"].data_ptr(), B, L, V, s, 1)
         self._run(pl.bwd_dec)
-        nz = B * G * A
-        buf["dzf"][:nz].copy_(buf["dzb"][:nz])
-        lib.concrete_bwd(buf["s"].data_ptr(), buf["z"].data_ptr(), buf["dzf"].data_ptr(), buf["gkl"].data_ptr(),
-                         buf["dlogits"].data_ptr(), B, G, A, float(temperature), tp, s)
-        buf["dlogitsb"][:nz].copy_(buf["dlogits"][:nz])
+        lib.concrete_bwd(buf["s"].data_ptr(), buf["z"].data_ptr(), buf["dzb"].data_ptr(), buf["gkl"].data_ptr(),
+                         buf["dlogitsb"].data_ptr(), B, G, A, float(temperature), tp, s, 1)
         self._run(pl.bwd_enc)
         if update and pl.skip is not None:
             lib.adam_update(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),

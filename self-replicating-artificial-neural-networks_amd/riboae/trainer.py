@@ -119,50 +119,86 @@ def train(experiment_name: str, model, train_tokens: np.ndarray, vocabulary, out
         opt.load_state_dict(ck["optimizer"])                    # either engine reads either format
     if bf16 is None:
         bf16 = dev.type == "cuda"
+    # the token dataset lives on the device for the HIP engine (int32, the kernels' token type): a batch is a view,
+    # not a host slice + upload per step
     data = torch.as_tensor(np.asarray(train_tokens), dtype=torch.long)
+    if hip is not None:
+        data = data.to(dev, torch.int32)
     n = len(data)
     nb = max(1, math.ceil(n / batch_size))
     history = []
     b = start
     t0 = time.perf_counter()
+    # The step's loss is read back one step late (HIP engine): the host enqueues step b before it waits for step
+    # b - 1's loss, so the GPU does not idle on the host between steps.  A backup of step b - 1 must hold step b - 1's
+    # weights, so while b - 1 is far enough from the last backup to be backed up, its loss is read (and the backup
+    # taken) before step b is enqueued; the decisions are the reference's (training.py:92-101), step for step.
+    pending = None                     # (step, metrics) whose loss has not been read yet
+
+    def settle(step_, metrics_):
+        nonlocal min_loss, min_loss_batch, t0
+        loss_ = float(metrics_["loss"].detach())
+        history.append(loss_)
+        if step_ % log_every == 0:
+            log(f'Batch: {step_} | Loss: {loss_:.5f} | NLL: {float(metrics_["nll"].detach()):.5f} | '
+                f'KL: {float(metrics_["kld"].detach()):.5f} '
+                f'| {(time.perf_counter() - t0) / log_every * 1e3:.1f} ms/batch')
+            t0 = time.perf_counter()
+        return loss_
+
+    def backup(step_, loss_):
+        nonlocal min_loss, min_loss_batch
+        path = os.path.join(out_dir, f"{experiment_name}_b{step_}.pt")
+        log("Backing up to: ", path)
+        save_checkpoint(path, model, "concrete" if is_concrete else "deterministic", step_, opt.state_dict(),
+                        {"loss": loss_})
+        prev = os.path.join(out_dir, f"{experiment_name}_b{min_loss_batch}.pt")
+        if min_loss_batch > 0 and os.path.exists(prev) and prev != path:
+            os.remove(prev)
+        min_loss, min_loss_batch = loss_, step_
+
     while max_steps is None or b < start + max_steps:
         i = (b - 1) % nb
-        x = data[i * batch_size:(i + 1) * batch_size].to(dev, non_blocking=True)
+        x = data[i * batch_size:(i + 1) * batch_size]
+        if x.device != dev:
+            x = x.to(dev, non_blocking=True)
         temperature, lr, kw = temperature_at(b), learning_rate_at(b), kld_weight_at(b)
         if hip is not None:
+            # a backup of step b - 1 must see step b - 1's weights: when b - 1 may be backed up (its distance to
+            # the last backup allows it), its loss is settled before step b is enqueued
+            if pending is not None and pending[0] - min_loss_batch >= min_backup_interval:
+                loss = settle(*pending)
+                if loss < min_loss:
+                    backup(pending[0], loss)
+                pending = None
             metrics = hip.step(x, temperature, kw, lr)
+            if pending is not None:
+                settle(*pending)        # (b - 1 could not be backed up: reading its loss now costs nothing)
+            pending = (b, metrics)
         else:
             with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=bool(bf16)):
                 metrics = model.compute_loss(x, temperature, kw) if is_concrete else model.compute_loss(x)
             opt.zero_grad()
             metrics["loss"].float().backward()
             opt.step(lr)
+            loss = settle(b, metrics)
+            if loss < min_loss and b - min_loss_batch >= min_backup_interval:
+                backup(b, loss)
         model._param_version = getattr(model, "_param_version", 0) + 1
-        loss = float(metrics["loss"].detach())
-        history.append(loss)
-        if b % log_every == 0:
-            log(f'Batch: {b} | Loss: {loss:.5f} | NLL: {float(metrics["nll"].detach()):.5f} | KL: {float(metrics["kld"].detach()):.5f} '
-                f'| {(time.perf_counter() - t0) / log_every * 1e3:.1f} ms/batch')
-            t0 = time.perf_counter()
         if vocabulary is not None and demo_every and b % demo_every == 0:
             model.eval()
             with torch.no_grad():
-                z = model.encode(x[:1])
+                z = model.encode(x[:1].long())
                 seq = model.decode(z).cpu().numpy()
             model.train()
             log(f"\n\nOriginal: \n{vocabulary.decode(x[:1].cpu().numpy())[0]}\n\n")
             log(f"Genotype:\n{''.join(str(int(v)) for v in z[0].cpu().numpy())}\n\n")
             log(f"Reconstruction: \n{vocabulary.decode(seq)[0]}\n\n")
-        if loss < min_loss and b - min_loss_batch >= min_backup_interval:
-            path = os.path.join(out_dir, f"{experiment_name}_b{b}.pt")
-            log("Backing up to: ", path)
-            save_checkpoint(path, model, "concrete" if is_concrete else "deterministic", b, opt.state_dict(),
-                            {"loss": loss})
-            prev = os.path.join(out_dir, f"{experiment_name}_b{min_loss_batch}.pt")
-            if min_loss_batch > 0 and os.path.exists(prev) and prev != path:
-                os.remove(prev)
-            min_loss, min_loss_batch = loss, b
         b += 1
+    if pending is not None:
+        loss = settle(*pending)
+        if loss < min_loss and pending[0] - min_loss_batch >= min_backup_interval:
+            backup(pending[0], loss)
     if max_steps is not None and b - 1 != min_loss_batch:
         # bounded runs always leave a final checkpoint (the reference loop never ends)
         path = os.path.join(out_dir, f"{experiment_name}_b{b - 1}.pt")

@@ -547,8 +547,7 @@ def _adam_run(mode, steps, grads, p0):
     p = p0.clone()
     m16 = mode == H.MOM_16
     m = torch.zeros(n, dtype=torch.bfloat16 if m16 else torch.float32, device="cuda")
-    v = (torch.full((n,), -32768, dtype=torch.int16, device="cuda") if m16
-         else torch.zeros(n, dtype=torch.float32, device="cuda"))
+    v = torch.zeros(n, dtype=torch.int16 if m16 else torch.float32, device="cuda")
     pbf = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
     step = torch.zeros(1, dtype=torch.int32, device="cuda")
     lr_t = torch.zeros(1, device="cuda")
