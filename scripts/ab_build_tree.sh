@@ -1,22 +1,26 @@
 #!/bin/bash
-# Build the HIP extension of the WORKING TREE into OUTDIR, after applying an optional sed expression to
-# common.h (timing experiments, e.g. plain stores in place of the fixed-point atomics):
-#   SED='s/atomicAdd(reinterpret_cast<u64_t\*>(p), (u64_t)fx_q(v));/*p = fx_q(v);/' bash scripts/ab_build_tree.sh ab/plain
+# Build the HIP extension of the WORKING TREE with extra compile flags into OUTDIR (SERANN_NATIVE_DIR A/B runs of
+# build-time knobs):  ABFLAGS="-DSERANN_DIVERGE_CHECK=0" bash scripts/ab_build_tree.sh ab/nochk
 set -e
 OUT=$1
-SRC=$(mktemp -d)
-cp -r self-replicating-artificial-neural-networks_amd/csrc/hip "$SRC/hip"
-D=$SRC/hip
-[ -n "$SED" ] && sed -i "$SED" "$D/common.h"
+D=self-replicating-artificial-neural-networks_amd/csrc/hip
+TMP=$(mktemp -d)
 mkdir -p "$OUT"
 SUF=$(python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
 PYI=$(python3 -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBI=$(python3 -c "import pybind11;print(pybind11.get_include())")
+CC="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Wno-unused-result $ABFLAGS -I$D -I$PYI -I$PBI"
 for f in "$D"/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 -Wno-unused-result $ABFLAGS \
-    -I"$D" -I"$PYI" -I"$PBI" -c "$f" -o "$SRC/$(basename "$f" .hip).o" &
+  b=$(basename "$f" .hip)
+  if [ "$b" = gemm3 ]; then
+    for p in 0 1 2 3; do $CC -DGEMM3_PART=$p -c "$f" -o "$TMP/${b}_p$p.o" & done
+  elif [ "$b" = gchain ]; then
+    $CC -mllvm -amdgpu-mfma-vgpr-form -c "$f" -o "$TMP/$b.o" &
+  else
+    $CC -c "$f" -o "$TMP/$b.o" &
+  fi
 done
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "$SRC"/*.o -o "$OUT/serann_hip$SUF"
-rm -rf "$SRC"
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "$TMP"/*.o -o "$OUT/serann_hip$SUF"
+rm -rf "$TMP"
 echo "built $OUT/serann_hip$SUF"

@@ -128,7 +128,10 @@ __device__ __forceinline__ double fxw_sum_d(const long long* ws, int C, int idx)
 // (fertility 0, as for an invalid organism).  org_off: int64 [norg + 1] first arena element of each organism
 // (ascending; the parameter arena is laid out organism by organism); diverged: int32 [norg].
 constexpr float FX_DIVERGE = 65504.f;
-__device__ __noinline__ void flag_diverged(const int64_t* __restrict__ org_off, int* __restrict__ diverged, int norg,
+#ifndef SERANN_DIVERGE_CHECK
+#define SERANN_DIVERGE_CHECK 1      // build-time A/B knob of the fused WGRAD epilogues' check
+#endif
+__device__ __forceinline__ void flag_diverged(const int64_t* __restrict__ org_off, int* __restrict__ diverged, int norg,
                                            int64_t e) {
     int lo = 0, hi = norg - 1;                       // the last organism whose first element is <= e
     while (lo < hi) {

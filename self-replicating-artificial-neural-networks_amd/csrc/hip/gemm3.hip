@@ -631,7 +631,7 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
     bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
     const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
     auto chk = [&](float gq, int64_t e) {            // common.h flag_diverged
-        if (ac.org_off && fabsf(gq) > FX_DIVERGE)
+        if (SERANN_DIVERGE_CHECK && ac.org_off && fabsf(gq) > FX_DIVERGE)
             flag_diverged(reinterpret_cast<const int64_t*>(ac.org_off), reinterpret_cast<int*>(ac.diverged), (int)ac.norg, e);
     };
     if (stage != nullptr) {

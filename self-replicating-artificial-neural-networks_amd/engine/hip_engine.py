@@ -758,6 +758,9 @@ class HipPopulationEngine(PopulationEngine):
             if not rows:
                 return
             assert len(rows) == len(dims), (len(rows), len(dims))
+            # split WGRADs of every variant group of this call are finalized by ONE grouped launch after the
+            # last of them (not one per group: a finalize launch is mostly its own latency)
+            wfin_all = []
             for v, rws, tiles in H.gemm3_plan(mode_, rows, dims, splitk=True):
                 if not len(tiles):
                     continue
@@ -793,11 +796,12 @@ class HipPopulationEngine(PopulationEngine):
                                                       int(r["N"]), int(r.get("ldo") or r["N"])))
                 plan.launches.append(Launch("gemm3", (mode_, v), desc_tensor(rws, H.GEMM_DTYPE), T(tiles),
                                             len(tiles)))
-                if wfin:
-                    add_chunked("wgfin", 0, wfin, H.WGFIN_DTYPE, [f["M"] * f["N"] for f in wfin], H.WGFIN_ELEMS)
+                wfin_all += wfin
                 if fin:
                     add_chunked("splitfin", 0, fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in fin],
                                 H.SPLITFIN_ELEMS)
+            if wfin_all:
+                add_chunked("wgfin", 0, wfin_all, H.WGFIN_DTYPE, [f["M"] * f["N"] for f in wfin_all], H.WGFIN_ELEMS)
             if extra_fin:
                 # K slices of fused-concat consumers (every variant launched above): one finalize
                 add_chunked("splitfin", 0, extra_fin, H.SPLITFIN_DTYPE, [f["M"] * f["N"] for f in extra_fin],

@@ -63,7 +63,7 @@ def _oracle_dev(ir, params, x, g, y, device, dtype):
     return grads
 
 
-def _check_vs_torch_bf16(name, B, seed):
+def _check_vs_torch_bf16(name, B, seed, perturbed_bound=None):
     from serann.engine.hip_engine import HipPopulationEngine
     ir = interpret(ARCHS[name])
     params = init_params(ir, 7)
@@ -80,11 +80,17 @@ def _check_vs_torch_bf16(name, B, seed):
     # to fp32 as torch's -- Dense(24) pre-activations 3.3e-3 relative for both -- but it lands four units on
     # the other side of zero, 5.8 % on the first Conv1D kernel against torch's 1.9 %; profiles/r5/
     # relu_knife_edge.txt).  The bound is the worse of the two references.
-    rng = np.random.default_rng(1000 + seed)
-    params2 = {nid: {k: (v * (1 + 2.0 ** -9 * rng.choice([-1.0, 1.0], size=v.shape))).astype(v.dtype)
-                     if k in ("kernel", "bias", "gamma", "beta") else v for k, v in d.items()}
-               for nid, d in params.items()}
-    bf2 = _oracle_dev(ir, params2, x, g, y, "cuda", torch.bfloat16)
+    # (B = 96 only, where the knife-edge analysis applies: at the production batch the single reference bounds)
+    if perturbed_bound is None:
+        perturbed_bound = B < 750
+    if perturbed_bound:
+        rng = np.random.default_rng(1000 + seed)
+        params2 = {nid: {k: (v * (1 + 2.0 ** -9 * rng.choice([-1.0, 1.0], size=v.shape))).astype(v.dtype)
+                         if k in ("kernel", "bias", "gamma", "beta") else v for k, v in d.items()}
+                   for nid, d in params.items()}
+        bf2 = _oracle_dev(ir, params2, x, g, y, "cuda", torch.bfloat16)
+    else:
+        bf2 = bf
     hip = eng.export_arena(0, grads)
     gmax = max(float(np.abs(v).max()) for d in ref.values() for v in d.values())
     for nid, d in ref.items():
@@ -592,9 +598,11 @@ def test_adam_16bit_moments_track_fp32_moments():
 
 
 def test_fit_16bit_moments_vs_fp32_moments():
-    """A 2-epoch fit (>= 50 graph-replayed Adam steps, 4 stream groups, fused-Adam WGRAD epilogues) with 16-bit
-    moments against the same fit with fp32 moments: weight displacements agree to a few percent of their size and
-    the validation accuracies to 0.05 (the reference itself keeps fp16 moments)."""
+    """Fits (graph replay, 4 stream groups, fused-Adam WGRAD and finalize epilogues; 4 epochs = 132 Adam steps) with
+    16-bit moments against the same fits with fp32 moments: every organism's validation accuracy within 0.03, the
+    population mean within 0.01.  (Mid-curve organisms after 2 epochs move by up to 0.26 under ANY perturbation --
+    fp32 moments with the learning rate x 1.001 as much as 16-bit moments: profiles/r6/moments_16bit_vs_fp32.txt --
+    so the comparison is made once they have converged.  The reference itself keeps fp16 moments.)"""
     from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
     from serann.engine.base import TrainConfig
     from serann.engine.hip_engine import HipPopulationEngine
@@ -602,24 +610,17 @@ def test_fit_16bit_moments_vs_fp32_moments():
                            n_train=8000, n_test=500)
     names = sorted(ARCHS)
     irs = [interpret(ARCHS[n]) for n in names]
-    runs = {}
+    acc = {}
     for mode in ("fp32", "16bit"):
-        cfg = TrainConfig(epochs=2, batch_size=256, adam_moments=mode)
+        cfg = TrainConfig(epochs=4, batch_size=256, adam_moments=mode, val_every_epoch=False)
         eng = HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
-        p0 = eng.p.clone()
         res = eng.fit(data, cfg)
-        assert res.steps >= 50
-        runs[mode] = (eng.p - p0, res, [eng.export_arena(i, eng.p - p0) for i in range(len(irs))])
-        assert (eng.m.dtype == torch.bfloat16) == (mode == "16bit")
+        assert res.steps >= 50 and (eng.m.dtype == torch.bfloat16) == (mode == "16bit")
+        acc[mode] = res.val_acc
         del eng
-    d32, r32, e32 = runs["fp32"]
-    d16, r16, e16 = runs["16bit"]
-    assert np.all(np.abs(r16.val_acc - r32.val_acc) < 0.05), (r16.val_acc, r32.val_acc)
-    for i, name in enumerate(names):
-        keys = [(k, w) for k in e32[i] for w in e32[i][k] if not w.startswith("moving")]
-        num = sum(float(np.linalg.norm(e16[i][k][w] - e32[i][k][w])) ** 2 for k, w in keys)
-        den = sum(float(np.linalg.norm(e32[i][k][w])) ** 2 for k, w in keys)
-        assert num ** 0.5 < 0.1 * den ** 0.5 + 1e-6, (name, num ** 0.5, den ** 0.5)
+    d = acc["16bit"] - acc["fp32"]
+    table = "\n".join(f"{n:30s} {a:.4f} {b:.4f}" for n, a, b in zip(names, acc["fp32"], acc["16bit"]))
+    assert np.all(np.abs(d) <= 0.03) and abs(d.mean()) <= 0.01, table
 
 
 def test_exploding_organism_is_flagged_diverged():
@@ -644,4 +645,43 @@ def test_exploding_organism_is_flagged_diverged():
     assert np.isfinite(res.val_acc[0]) and np.isnan(res.val_acc[1]) and np.isnan(res.val_mse[1])
     acc = eng.evaluate(data.test_x, data.test_labels, data.test_g, cfg)
     assert np.isfinite(acc[0]) and np.isnan(acc[1])
+    eng.close()
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid"])
+def test_bn_statistics_of_a_far_from_zero_input(act):
+    """GF_BNUSTAT sums the producer's stored bf16 outputs unshifted (fp32 per wave, then wide fixed point,
+    finished in double: gemm3.hip bn_ustat_flush).  On a BatchNormalization input whose mean is ~100x its spread
+    (a Dense with bias 100, or a saturated sigmoid) the batch mean and inverse std the engine uses match a two-pass
+    computation over the very same stored bf16 tensor."""
+    from serann.engine.hip_engine import HipPopulationEngine
+    src = ("X_layer = Conv2D(filters=48, kernel_size=3, strides=2)(X_layer)\n"
+           f"X_layer = Dense(units=24, activation='{act}')(X_layer)\nX_layer = BatchNormalization()(X_layer)\n\n"
+           "g_layer = Dense(units=16, activation='relu')(g_layer)\n\n"
+           "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
+           "con = Dense(units=40, activation='relu')(con)\n\nloss_balance = 0.4")
+    ir = interpret(src)
+    params = init_params(ir, 3)
+    dense = next(n for n in ir.nodes if n.op == "gemm" and n.attrs["kind"] != "head_cls" and n.attrs["cin"] == 48)
+    bn = next(n for n in ir.nodes if n.op == "bn")
+    params[dense.id]["bias"] = np.full_like(params[dense.id]["bias"], 100.0 if act == "relu" else 6.0)
+    x, g, y = _batch(750, seed=5)
+    eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    eng.debug_train_step(x, g, y)
+    mem = eng._debug_mem
+    rec = mem["orgs"][0]
+    C = bn.attrs["channels"]
+    _, off = rec["act"][dense.id]
+    import math
+    xin = mem["act"].view(off, 750 * math.prod(dense.shape)).view(-1, C).double().cpu()   # the stored bf16 BN input
+    # (the LDS-tiled 1x1 FWD with the BN statistics in its epilogue: a Dense over 48 channels, no k splits)
+    f32 = mem["f32"]
+    mean = f32.view(rec["bn"][bn.id]["mean"], C).double().cpu()
+    invstd = f32.view(rec["bn"][bn.id]["invstd"], C).double().cpu()
+    want_mean = xin.mean(0)
+    want_var = ((xin - want_mean) ** 2).mean(0)                              # two-pass
+    assert float((xin.std(0) / xin.mean(0).abs()).max()) < 0.05            # |mean| / std > 20 on every channel
+    assert torch.allclose(mean, want_mean, rtol=1e-6, atol=0)
+    want_invstd = 1.0 / torch.sqrt(want_var + 1e-3)
+    assert float(((invstd - want_invstd).abs() / want_invstd).max()) < 1e-3, (invstd, want_invstd)
     eng.close()
