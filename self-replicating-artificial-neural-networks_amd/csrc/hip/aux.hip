@@ -963,6 +963,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
         float* P = reinterpret_cast<float*>(ac->p);
         void* Mo = reinterpret_cast<void*>(ac->m);
         void* Vo = reinterpret_cast<void*>(ac->v);
+        bf16_t* Pb = reinterpret_cast<bf16_t*>(ac->pbf);    // (read before the stores below)
         const bool m16 = ac->mode == MOM_16;
         if (ac->org_off && fabsf(fx_f(q)) > FX_DIVERGE)
             flag_diverged(reinterpret_cast<const int64_t*>(ac->org_off), reinterpret_cast<int*>(ac->diverged),
@@ -974,7 +975,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
         P[pe] = p_;
         if (m16) { m_st<MOM_16>(Mo, pe, m_); v_st<MOM_16>(Vo, pe, v_); }
         else { m_st<MOM_F32>(Mo, pe, m_); v_st<MOM_F32>(Vo, pe, v_); }
-        reinterpret_cast<bf16_t*>(ac->pbf)[pe] = f2bf(p_);
+        Pb[pe] = f2bf(p_);
     }
 }
 

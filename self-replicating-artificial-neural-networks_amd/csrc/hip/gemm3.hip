@@ -623,16 +623,20 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
     const int c16 = lane & 15, rq = (lane >> 4) * 4;
     const long long* out = reinterpret_cast<const long long*>(d.out);
     const int ldo = d.ldo ? (int)d.ldo : g.N;
-    const AdamCtx& ac = *reinterpret_cast<const AdamCtx*>(d.adam);
+    // every AdamCtx field is read into registers here, before the first store: read through the struct inside
+    // the pass loop, each field would be re-loaded after every p / m / v store the compiler cannot prove disjoint
+    const AdamCtx ac = *reinterpret_cast<const AdamCtx*>(d.adam);
     const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
     float* __restrict__ P = reinterpret_cast<float*>(ac.p);
     void* __restrict__ Mo = reinterpret_cast<void*>(ac.m);
     void* __restrict__ Vo = reinterpret_cast<void*>(ac.v);
     bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
     const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
+    const int64_t* __restrict__ org_off = reinterpret_cast<const int64_t*>(ac.org_off);
+    int* __restrict__ diverged = reinterpret_cast<int*>(ac.diverged);
+    const int norg = (int)ac.norg;
     auto chk = [&](float gq, int64_t e) {            // common.h flag_diverged
-        if (SERANN_DIVERGE_CHECK && ac.org_off && fabsf(gq) > FX_DIVERGE)
-            flag_diverged(reinterpret_cast<const int64_t*>(ac.org_off), reinterpret_cast<int*>(ac.diverged), (int)ac.norg, e);
+        if (SERANN_DIVERGE_CHECK && org_off != nullptr && fabsf(gq) > FX_DIVERGE) flag_diverged(org_off, diverged, norg, e);
     };
     if (stage != nullptr) {
         // Row-major through LDS (stage: 2 x TR x LD floats; the k loop's tiles are dead): a lane of the
@@ -645,8 +649,30 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
         const bool vec = (t0 & 3) == 0 && (ldo & 3) == 0;      // float4-aligned rows
         const int cg = lane % CG, rr = lane / CG;
         const int col = kcol0 + cg * 4;
-        // (issuing every pass's p / m / v loads ahead of the LDS rounds -- one round trip instead of TR / RPI --
-        // measured 30 % slower on the ancestor step: the prefetch registers cost the k loop its occupancy)
+        // Software-pipelined one row pass deep: the p / m / v loads of pass it + 1 are issued before pass it's
+        // stores (different rows; the compiler cannot hoist them itself over stores through possibly aliasing
+        // pointers), and every wave issues its first pass's loads before the LDS rounds, so the second round's
+        // loads fly during the first.  (Issuing ALL passes' loads up front -- one round trip -- measured 30 %
+        // slower on the ancestor step: those registers cost the k loop its occupancy.)
+        using MT = typename std::conditional<MM == MOM_16, uint2, float4>::type;
+        const bool vcol = vec && col + 4 <= g.N;
+        auto ld_pass = [&](int it, float4& pp, MT& mm, MT& vv) {
+            const int row = frow0 + it * RPI + rr;
+            if (vcol && row < g.M) {
+                const int64_t e = e0 + (int64_t)row * ldo + col;
+                pp = *reinterpret_cast<const float4*>(&P[e]);
+                if constexpr (MM == MOM_16) {
+                    mm = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(Mo) + e);
+                    vv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(Vo) + e);
+                } else {
+                    mm = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Mo) + e);
+                    vv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Vo) + e);
+                }
+            }
+        };
+        float4 pn;
+        MT mn, vn;
+        ld_pass(0, pn, mn, vn);
         for (int half = 0; half < 2; ++half) {
             __syncthreads();
             if ((wave >> 1) == half) {
@@ -661,15 +687,24 @@ __device__ __forceinline__ void wgrad_adam_flush(const GemmDesc& d, const G3& g,
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 for (int it = 0; it < TR / RPI; ++it) {
+                    float4 p4 = pn;
+                    const MT mr = mn, vr = vn;
+                    if (it + 1 < TR / RPI) ld_pass(it + 1, pn, mn, vn);
                     const int row = frow0 + it * RPI + rr;
                     if (row >= g.M || col >= g.N) continue;
                     const float4 gv = *reinterpret_cast<const float4*>(&st[(it * RPI + rr) * LD + cg * 4]);
                     const int64_t e = e0 + (int64_t)row * ldo + col;
                     chk(fmaxf(fmaxf(fabsf(gv.x), fabsf(gv.y)), fmaxf(fabsf(gv.z), fabsf(gv.w))), e);
-                    if (vec && col + 4 <= g.N) {
-                        float4 p4 = *reinterpret_cast<const float4*>(&P[e]);
-                        float4 m4 = m_ld4<MM>(Mo, e);
-                        float4 v4 = v_ld4<MM>(Vo, e);
+                    if (vcol) {
+                        float4 m4, v4;
+                        if constexpr (MM == MOM_16) {
+                            m4 = make_float4(__uint_as_float(mr.x << 16), __uint_as_float(mr.x & 0xffff0000u),
+                                             __uint_as_float(mr.y << 16), __uint_as_float(mr.y & 0xffff0000u));
+                            v4 = make_float4(log16_f(vr.x), log16_f(vr.x >> 16), log16_f(vr.y), log16_f(vr.y >> 16));
+                        } else {
+                            m4 = mr;
+                            v4 = vr;
+                        }
                         adam_elem(p4.x, m4.x, v4.x, fx_f(fx_q(gv.x)), lr_t, ac.b1, ac.b2, ac.eps);
                         adam_elem(p4.y, m4.y, v4.y, fx_f(fx_q(gv.y)), lr_t, ac.b1, ac.b2, ac.eps);
                         adam_elem(p4.z, m4.z, v4.z, fx_f(fx_q(gv.z)), lr_t, ac.b1, ac.b2, ac.eps);
@@ -2343,7 +2378,11 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
     // swizzled k-chunk offsets (elements) of this lane's fragment reads and of its staging stores
     auto kswz = [](int row, int chunk) { return (chunk ^ ((0x1320 >> (((row >> 2) & 3) * 4)) & 3)) << 3; };
     const int kfa = kswz(r16, lane >> 4);
-    const int m0 = td.y * BM, n0 = td.z * BN;
+    // td.z: first n tile | (n tiles of this block << 16): a block walks ntc consecutive column tiles of its row tile
+    // (the tiles are independent -- each output tile is one block's -- so the grouping is a schedule choice only)
+    const int m0 = td.y * BM;
+    int n0 = (td.z & 0xffff) * BN;
+    const int ntc = max(1, td.z >> 16);
     const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;
     const int64_t a_elems = (int64_t)M * lda;
     const rsrc_t rA = mkrsrc(d.a, a_elems * 2);
@@ -2420,6 +2459,9 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         }
     };
 
+    bool pre = false;
+    for (int nti = 0; nti < ntc; ++nti, n0 += BN) {
+    if (nti > 0) __syncthreads();                    // the previous tile's epilogue is done with the LDS
     f32x4_t acc[4][NTW];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -2427,13 +2469,22 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
         for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     if (kt0 < kt1) {
-        gload(kt0);
-        sstore(0);
+        if (!pre) gload(kt0);                        // (pre: this tile's first k step was loaded during the
+        sstore(0);                                   //  previous tile's epilogue)
     }
+    pre = false;
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
         const int buf = (kt - kt0) & 1;
-        if (kt + 1 < kt1) gload(kt + 1);
+        if (kt + 1 < kt1) {
+            gload(kt + 1);
+        } else if (nti + 1 < ntc) {
+            // last k step: the next n tile's first k step goes in flight now, across this tile's epilogue
+            n0 += BN;
+            gload(kt0);
+            n0 -= BN;
+            pre = true;
+        }
         Frag fa[4], fb[NTW];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -2610,7 +2661,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
                 if (n2 < N) part[(int64_t)n2 * NSUM + q] = v;
             }
         }
-        return;
+        continue;
     }
     if (MODE == MODE_FWD && (flags & GF_SPLITWS)) {
         // raw fp32 partial of this k split; splitk_finalize adds the splits, bias and activation
@@ -2627,7 +2678,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
                     if (row < M) w[(int64_t)row * N + col] = acc[i][j][r];
                 }
         }
-        return;
+        continue;
     }
     if (flags & GF_OUT_F32) {
         float* o = reinterpret_cast<float*>(d.out);
@@ -2645,7 +2696,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
                     o[(int64_t)row * N + col] = apply_act(acc[i][j][r] + bv, oact);
                 }
         }
-        return;
+        continue;
     }
     bf16_t* o = reinterpret_cast<bf16_t*>(d.out);
     const bool accum = (flags & GF_ACCUM) != 0;
@@ -2683,7 +2734,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             if (accum) v += bf2f(dst[e]);
             dst[e] = f2bf(v);
         }
-        return;
+        continue;
     }
     {
         // general tile (wide outputs: DGRAD of a merged Dense, FWD with N > BN): the tile is staged in LDS
@@ -2731,6 +2782,7 @@ __global__ __launch_bounds__(256) void g3_tiled_kernel(const GemmDesc* __restric
             }
         }
     }
+    }   // n tiles
 }
 
 // variant encoding (FWD / DGRAD): NT (BN/16: 1, 2, 4, 8) + 10 * RT (2 or 4) + 100 * KW + 1000 * GEN,

@@ -896,7 +896,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                     if ns > 1 or r.get("_ws"):
                         r["kper"] = max(per, 1)
                         r["flags"] = int(r.get("flags", 0)) | GF_SPLITWS
-                    t = gemm_tiles([(M, N, K)], mode, bm=bm, bn=bn)
+                    t = gemm_tiles([(M, N, K)], mode, bm=bm, bn=bn, ngroup=tiled_ngroup(items, bm, bn))
                     spl = []
                     for s_ in range(ns):
                         k0, k1 = s_ * per, min(kt, (s_ + 1) * per)
@@ -911,7 +911,9 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                         tl.append(xcd_swizzle(np.concatenate(spl), len(t)))
                 tiles = np.concatenate(tl).astype(np.int32) if tl else np.zeros((0, 4), np.int32)
             else:
-                tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000)
+                tiled = 7000 <= v < 9000 or 17000 <= v < 19000
+                tiles = gemm_tiles(dms, mode, bm=bm, bn=bn, swizzle=mode == MODE_DGRAD and v >= 7000,
+                                   ngroup=tiled_ngroup(items, bm, bn) if tiled else 1)
         out.append((v, [r for r, _ in items], tiles))
     return out
 
@@ -1051,17 +1053,39 @@ WGRAD_SLABS = _os.environ.get("SERANN_WGRAD_SLABS", "1") != "0"
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
 
 
+# LDS-tiled FWD / DGRAD: n tiles per block (g3_tiled_kernel walks them in turn) when a launch has at least
+# TILED_NGROUP_MIN tiles -- tens of thousands of 5-k-step blocks (the ancestor's merged-Dense DGRAD: 44,250) spend
+# their time in block prologues and epilogues (profiles/r5/ab_nbnsum_epilogue_sums.txt)
+TILED_NGROUP = int(_os.environ.get("SERANN_TILED_NGROUP", "4"))
+TILED_NGROUP_MIN = int(_os.environ.get("SERANN_TILED_NGROUP_MIN", "4096"))
+
+
+def tiled_ngroup(items, bm: int, bn: int) -> int:
+    """n tiles per block of one LDS-tiled launch (``items``: its (row, (M, N, K)) problems; k splits included)."""
+    if TILED_NGROUP <= 1:
+        return 1
+    total = 0
+    for r, (M, N, K) in items:
+        total += -(-int(M) // bm) * -(-int(N) // bn) * max(1, int(r.get("_split", 1)))
+    return TILED_NGROUP if total >= TILED_NGROUP_MIN else 1
+
+
 def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int = BM,
-               bn: int = BN, swizzle: bool = False) -> np.ndarray:
+               bn: int = BN, swizzle: bool = False, ngroup: int = 1) -> np.ndarray:
     """dims: list of (M, N, K) per problem -> int32 (ntiles, 4) table (prob, tm, tn, kt0|kt1<<16).
     target_ksteps: int, or one value per problem (WGRAD m-split granularity).  Vectorised over the k
-    splits of a problem (a WGRAD over 432k rows has hundreds): plans are rebuilt every generation."""
+    splits of a problem (a WGRAD over 432k rows has hundreds): plans are rebuilt every generation.
+    ``ngroup`` > 1 (LDS-tiled kernel): a block walks up to ngroup consecutive n tiles of its row tile; the n entry
+    is then first tile | (tiles << 16)."""
     rows = []
     for p, (M, N, K) in enumerate(dims):
         tm, tn = -(-M // bm), -(-N // bn)
         kt = -(-K // BK)
         if tm == 0 or tn == 0:
             continue
+        ng = max(1, min(int(ngroup), tn))
+        tn_full = tn
+        tn = -(-tn_full // ng)                      # n groups
         nsplit = 1
         tgt = target_ksteps[p] if isinstance(target_ksteps, (list, tuple)) else target_ksteps
         if mode == MODE_WGRAD:
@@ -1076,7 +1100,8 @@ def gemm_tiles(dims, mode: int, target_ksteps=128, min_ksteps: int = 32, bm: int
         blk = np.empty((len(packed), T, 4), np.int64)
         blk[:, :, 0] = p
         blk[:, :, 1] = idx % tm
-        blk[:, :, 2] = idx // tm
+        g = idx // tm
+        blk[:, :, 2] = g * ng if ng == 1 else (g * ng) | (np.minimum(ng, tn_full - g * ng) << 16)
         blk[:, :, 3] = packed[:, None]
         if swizzle:
             # m fastest: the tm tiles of one n column share its B panel (WGRAD: the X columns,

@@ -55,6 +55,10 @@ class _Plan:
     """Buffers and launch lists of one batch size."""
 
 
+# attributes _build_buffers sets (one set per batch size, shared by the fused and unfused plans)
+_BUF_ATTRS = ("geo", "shapes", "flat", "gflat", "buf", "wt", "wsa", "mean", "invstd")
+
+
 class HipRiboTrainer:
     def __init__(self, model, device="cuda", beta1=0.9, beta2=0.999, eps=1e-7, ksplit: int = 32):
         self.model = model
@@ -72,6 +76,7 @@ class HipRiboTrainer:
         self.L, self.E, self.G, self.A, self.V = inf.max_len, inf.emb_dim, inf.genotype_length, inf.alphabet, gen.vocab
         self._build_params()
         self.plans: Dict[int, _Plan] = {}
+        self._bufs: Dict[int, dict] = {}             # per batch size: the buffers both plans of that size use
         self.keep: List[torch.Tensor] = []          # split-WGRAD slabs referenced by the launch descriptors
 
     def _plan(self, B: int, fused: bool = False) -> _Plan:
@@ -83,7 +88,14 @@ class HipRiboTrainer:
             self.B = int(B)
             self.fused_adam = bool(fused) and self.fuse_adam
             self.adam_regions = []
-            self._build_buffers()
+            # the fused and unfused plans of one batch size share every buffer (only their WGRAD descriptors
+            # differ): a debug_grads / update=False call after training allocates no second activation set
+            if int(B) in self._bufs:
+                for k, v in self._bufs[int(B)].items():
+                    setattr(self, k, v)
+            else:
+                self._build_buffers()
+                self._bufs[int(B)] = {k: getattr(self, k) for k in _BUF_ATTRS}
             self._build_launches()
             pl = _Plan()
             for k in ("buf", "wsa", "mean", "invstd", "fwd_enc", "fwd_dec", "bwd_dec", "bwd_enc", "trans", "wt"):

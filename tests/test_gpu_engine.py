@@ -664,9 +664,12 @@ def test_bn_statistics_of_a_far_from_zero_input(act):
     params = init_params(ir, 3)
     dense = next(n for n in ir.nodes if n.op == "gemm" and n.attrs["kind"] != "head_cls" and n.attrs["cin"] == 48)
     bn = next(n for n in ir.nodes if n.op == "bn")
-    params[dense.id]["bias"] = np.full_like(params[dense.id]["bias"], 100.0 if act == "relu" else 6.0)
     x, g, y = _batch(750, seed=5)
     eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    off = eng.layouts[0].b[dense.id]                 # (the engine initialises biases to zero, as Keras does)
+    with torch.no_grad():
+        eng.p[off:off + 24] = 100.0 if act == "relu" else 6.0
+        eng.pbf[off:off + 24] = eng.p[off:off + 24].to(torch.bfloat16)
     eng.debug_train_step(x, g, y)
     mem = eng._debug_mem
     rec = mem["orgs"][0]
@@ -685,3 +688,26 @@ def test_bn_statistics_of_a_far_from_zero_input(act):
     want_invstd = 1.0 / torch.sqrt(want_var + 1e-3)
     assert float(((invstd - want_invstd).abs() / want_invstd).max()) < 1e-3, (invstd, want_invstd)
     eng.close()
+
+
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "empty_x_branch", "nbn_sum_acts", "conv_pool_dense"])
+def test_tiled_n_tile_groups_are_bitwise_neutral(name, monkeypatch):
+    """LDS-tiled FWD / DGRAD blocks walking several n tiles (hip_ops.tiled_ngroup, forced on here for every launch)
+    give bitwise the logits and gradients of one tile per block: every output tile is still one block's."""
+    from serann.engine.hip_engine import HipPopulationEngine
+    from serann.ops import hip_ops as H
+    ir = interpret(ARCHS[name])
+    params = init_params(ir, 11)
+    x, g, y = _batch(750, seed=2)
+    out = []
+    for ng, mn in ((1, 1 << 30), (3, 1)):
+        monkeypatch.setattr(H, "TILED_NGROUP", ng)
+        monkeypatch.setattr(H, "TILED_NGROUP_MIN", mn)
+        eng = HipPopulationEngine([ir], [0], device="cuda", params=[params])
+        grads, metrics = eng.debug_train_step(x, g, y)
+        tiled = [la for la in eng._debug_plan.launches if la.kind == "gemm3" and 7000 <= la.arg[1] % 10000 < 9000]
+        out.append((grads.cpu(), eng.debug_logits()[0], metrics, len(tiled)))
+        eng.close()
+    (g1, l1, m1, n1), (g3, l3, m3, n3) = out
+    assert n1 > 0 and n3 == n1
+    assert torch.equal(g1, g3) and np.array_equal(l1, l3) and np.array_equal(m1, m3)

@@ -163,3 +163,22 @@ def test_checkpoint_moments_cross_engines(tmp_path):
     n = tr.pa.size
     assert int(tr2.step_i.item()) == 3
     assert torch.equal(tr2.m[:n].cpu(), tr.m[:n].cpu()) and torch.equal(tr2.v[:n].cpu(), tr.v[:n].cpu())
+
+
+def test_fused_and_unfused_plans_share_buffers():
+    """The training step's plan (fused Adam) and the debug / update=False plan of the same batch size share one set of
+    activation buffers and workspaces: a debug_grads call after training allocates no second set."""
+    from serann.riboae.hip_trainer import HipRiboTrainer
+    m = _model()
+    x, u = _batch()
+    tr = HipRiboTrainer(m, device="cuda")
+    tr.step(x, 0.3, 0.05, 1e-3, noise=u)
+    torch.cuda.synchronize()
+    before = torch.cuda.memory_allocated()
+    tr.debug_grads(x, 0.3, 0.05, u)
+    torch.cuda.synchronize()
+    assert len(tr.plans) == 2 and len(tr._bufs) == 1
+    pf, pu = tr.plans[(48, True)], tr.plans[(48, False)]
+    assert pf.buf is pu.buf and pf.mean is pu.mean
+    # (only the unfused plan's own descriptors, tile tables and split slabs are new)
+    assert torch.cuda.memory_allocated() - before < 16 << 20, torch.cuda.memory_allocated() - before
