@@ -1017,6 +1017,11 @@ def wgrad_target(M: int, N: int, K: int = 0, bm: int = 64, bn: int = 64, rg: int
     sharding)."""
     tg = _WGRAD_TARGET * rg
     tiles = -(-int(M) // bm) * -(-int(N) // bn)
+    if K and -(-int(K) // BK) <= WGRAD_NOSPLIT_KSTEPS:
+        # a short reduction (the batch-750 rows of a merged-Dense / head WGRAD) stays one split: its blocks walk
+        # 24 k steps either way, and the split cost a partial-sum round trip and the fused Adam epilogue (round 6:
+        # the ancestor's X-slice and head WGRADs; 13 % of the round-5 bench kernel time was such m-splits)
+        return max(tg, -(-int(K) // BK))
     while tg > 16 and K and tiles * wgrad_splits(K, tg, min(32, tg)) < WGRAD_MIN_BLOCKS // rg:
         tg //= 2
     return tg
@@ -1048,6 +1053,8 @@ DWGRAD = _os.environ.get("SERANN_DWGRAD", "0") != "0"
 DWGRAD_RG = int(_os.environ.get("SERANN_DWGRAD_RG", "2"))
 DWGRAD_CALIGN = int(_os.environ.get("SERANN_DWGRAD_CALIGN", "8"))
 WGRAD_MIN_BLOCKS = int(_os.environ.get("SERANN_WGRAD_MIN_BLOCKS", "32"))     # per problem (round 2: 64)
+# WGRAD reductions of at most this many 32-row k steps are never m-split (wgrad_target)
+WGRAD_NOSPLIT_KSTEPS = int(_os.environ.get("SERANN_WGRAD_NOSPLIT_KSTEPS", "32"))
 # Dense / 1x1 WGRAD m-splits meet in fp32 slabs + an ordered finalize (GF_WSLAB, round 6) instead of Q40 atomics
 WGRAD_SLABS = _os.environ.get("SERANN_WGRAD_SLABS", "1") != "0"
 _WGRAD_MAXSPLIT = int(_os.environ.get("SERANN_WGRAD_MAXSPLIT", "1000000"))
