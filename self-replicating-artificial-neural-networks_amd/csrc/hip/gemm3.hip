@@ -2165,7 +2165,10 @@ __global__ __launch_bounds__(256) void g3_narrow_fwd_sr_kernel(const GemmDesc* _
         }
     }
     const int64_t total = (int64_t)M * N;
-    const int r0 = td.y * NARROW_ROWS, r1 = min(M, r0 + NARROW_ROWS);
+    // rows per block: NARROW_ROWS, or d.kper (a multiple of 8) for a statistics-only pass (GF_NOSTORE: ~nothing to
+    // do per row, so the per-block weight setup and statistics flush would dominate 256-row blocks)
+    const int rpb = d.kper ? (int)d.kper : NARROW_ROWS;
+    const int r0 = td.y * rpb, r1 = min(M, r0 + rpb);
     const int sr0 = r0 / 8, sr1 = (r1 + 7) / 8;
     if (active) {
         constexpr int U = NARROW_SR_U;

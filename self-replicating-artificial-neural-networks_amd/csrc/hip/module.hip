@@ -28,6 +28,7 @@ static py::dict desc_sizes() {
     d["RepBitsDesc"] = sizeof(RepBitsDesc);
     d["NbnDesc"] = sizeof(NbnDesc);
     d["AdamCtx"] = sizeof(AdamCtx);
+    d["BinDesc"] = sizeof(BinDesc);
     return d;
 }
 
@@ -73,4 +74,5 @@ PYBIND11_MODULE(serann_hip, m) {
     m.def("cat_loglik_bwd", &launch_cat_loglik_bwd, py::arg("z"), py::arg("x"), py::arg("gout"), py::arg("dz"), py::arg("B"),
           py::arg("L"), py::arg("V"), py::arg("stream"), py::arg("bf16") = 0);
     m.def("onehot", &launch_onehot);
+    m.def("bin", &launch_bin);
 }

@@ -123,6 +123,8 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
 
 
 FUSE_NBN = os.environ.get("SERANN_FUSE_NBN", "1") != "0"
+# binary-genotype factorisation of raw-genotype Dense -> BN pairs read by a merged-Dense K slice (csrc/hip/bnbn.hip)
+BINARY_NBN = os.environ.get("SERANN_BINARY_NBN", "1") != "0"
 # fused pairs whose BN output feeds one LDS-tiled DGRAD: BN backward sums in that DGRAD's epilogue (nbn phase 6)
 NBN_SUM = os.environ.get("SERANN_NBNSUM", "1") != "0"
 
@@ -154,6 +156,26 @@ def nbn_pairs(ir: OrganismIR) -> Dict[int, int]:
             continue
         out[b.id] = n.id
     return out
+
+
+class _Deferred:
+    """A device address inside a buffer allocated later: element offset ``off`` (int64 words) plus a byte delta."""
+
+    def __init__(self, off: int, delta: int = 0):
+        self.off, self.delta = int(off), int(delta)
+
+    def __add__(self, nbytes: int) -> "_Deferred":
+        return _Deferred(self.off, self.delta + int(nbytes))
+
+    def resolve(self, base: int) -> int:
+        return int(base) + 8 * self.off + self.delta
+
+
+def _is_binary(a) -> bool:
+    """True when every element of the genotype array ``a`` is 0 or 1 (the factorised genotype-slice path's
+    precondition; the reference's genotypes always are)."""
+    arr = np.asarray(a)
+    return bool(arr.size) and bool(np.all((arr == 0) | (arr == 1)))
 
 
 def _padded_zeros(shape, dtype, device) -> torch.Tensor:
@@ -352,6 +374,10 @@ class Plan:
                 L.splitk_finalize(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
             elif k == "wgfin":
                 L.wgrad_finalize(la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "bin":
+                L.bin(la.arg, la.descs.data_ptr(), la.tiles.data_ptr(), la.n, s)
+            elif k == "memset":
+                L.memset32(la.arg[0], la.arg[1], s)
             else:
                 raise ValueError(k)
 
@@ -975,6 +1001,67 @@ class HipPopulationEngine(PopulationEngine):
                     if ok:
                         nbnsum[o].add(bid)
         nbnsum_rows = [dict() for _ in range(P)]
+        # binary-genotype pairs (bnbn.hip): an nbnsum pair on the raw genotype whose BN output is one K slice of a
+        # merged Dense -- the slice's FWD / DGRAD / WGRAD become the factorised kernels and its BN output is never
+        # written.  Only when this engine's genotype batches are binary (fit / debug_train_step check the data).
+        binpair = [dict() for _ in range(P)]           # bid -> consumer gemm id
+        if train and BINARY_NBN and getattr(self, "_g_binary", False):
+            for o, lay in org_iter():
+                ir = lay.ir
+                for bid in nbnsum[o]:
+                    did = nbn[o][bid]
+                    if ir.node(ir.node(did).inputs[0]).attrs["name"] != "g":
+                        continue
+                    own_ = mem["orgs"][o]["owner"]
+                    cons = [(g_, c_) for g_, c_ in fcons[o].items()
+                            if any(own_.get(pid, pid) == bid for pid, _, _ in fcat[o].get(c_, []))]
+                    if len(cons) != 1:
+                        continue
+                    cn = ir.node(cons[0][0])
+                    Lg, Fb = ir.genotype_size, ir.node(did).attrs["f"]
+                    if (cn.attrs["kind"] == "dense" and cn.attrs["f"] <= 256 and Lg <= 256 and Fb <= 256
+                            and math.prod(ir.node(bid).shape) == Lg * Fb):
+                        binpair[o][bid] = cons[0][0]
+
+        def binslice(o, pid, cid):
+            """The binary pair whose BN output is K slice ``pid`` (a concat input: the BN's reshape) of consumer
+            ``cid``, or None."""
+            bid = mem["orgs"][o]["owner"].get(pid, pid)
+            return bid if binpair[o].get(bid) == cid else None
+
+        def bin_desc(o, bid, cid, col, width):
+            """BinDesc of pair ``bid`` and its consumer ``cid`` (K slice at column ``col``), with its E / C0
+            workspaces; the FWD slab, the H / cs / part buffers and dW are filled in by the callers."""
+            lay_ = self.layouts[o]
+            ir_ = lay_.ir
+            did = nbn[o][bid]
+            Nc = ir_.node(cid).attrs["f"]
+            Lg, Fb = ir_.genotype_size, ir_.node(did).attrs["f"]
+            Ew = torch.empty(Lg * Nc + Nc, dtype=torch.float32, device=self.device)
+            plan.keep.append(Ew)
+            bd_ = mem["orgs"][o]["bn"][bid]
+            return dict(g=inputs[o]["g"], w=wptr_bf(lay_.w[did]), bias=pptr(lay_.b[did]) if did in lay_.b else 0,
+                        gamma=pptr(lay_.gamma[bid]) if bid in lay_.gamma else 0,
+                        beta=pptr(lay_.beta[bid]) if bid in lay_.beta else 0,
+                        mean=f32a.ptr(bd_["mean"]), invstd=f32a.ptr(bd_["invstd"]),
+                        act=H.ACT_CODES[ir_.node(did).attrs["act"]],
+                        flags=(1 if bid in lay_.gamma else 0) | (2 if bid in lay_.beta else 0),
+                        wc=wptr_bf(lay_.w[cid]) + 2 * col, ldw=ir_.node(cid).attrs["cin"], Nc=Nc, L=Lg, F=Fb, B=B,
+                        E=Ew.data_ptr(), C0=Ew.data_ptr() + 4 * Lg * Nc)
+
+        def add_bin(phase, rows):
+            if not rows:
+                return
+            if phase == 0:                             # (problem, n)
+                counts = [int(r["Nc"]) for r in rows]
+            elif phase == 1:                           # (problem, 32-row block)
+                counts = [-(-int(r["B"]) // 32) for r in rows]
+            elif phase == 3:                           # (problem, position)
+                counts = [int(r["L"]) for r in rows]
+            else:                                      # (problem, n)
+                counts = [int(r["Nc"]) for r in rows]
+            tiles = H.chunk_tiles(counts, 1)
+            plan.launches.append(Launch("bin", phase, desc_tensor(rows, H.BIN_DTYPE), T(tiles), len(tiles)))
 
         def nbnsum_ext(o, bid, M_, N_):
             """Device NbnDesc (with its partial-sum workspace) for the GF_NBNSUM DGRAD of pair ``bid``."""
@@ -1013,14 +1100,18 @@ class HipPopulationEngine(PopulationEngine):
                         R=R_, F=a_["f"], K=a_["cin"], ldx=a_["cin"], act=H.ACT_CODES[a_["act"]], flags=bflags,
                         eps=ba["epsilon"], momentum=ba["momentum"])
 
-        def add_nbn(rows, phase):
+        def add_nbn(rows, phase, stats_only=False):
             by_k: Dict[int, list] = {}
             for r in rows:
-                by_k.setdefault(int(r["K"]), []).append(r)
+                by_k.setdefault(int(r["K"]), []).append({k: v for k, v in r.items() if not k.startswith("_")})
             for k_ in sorted(by_k):
                 rws = by_k[k_]
-                tiles = H.nbn_fin_tiles([r["F"] for r in rws]) if phase == 6 else \
-                    H.nbn_tiles([(r["R"], r["F"]) for r in rws], phase)
+                if stats_only:
+                    # phase 2's first block of each problem only: statistics, moving averages, mean / invstd
+                    tiles = np.array([(p_, 0, 0, 1) for p_ in range(len(rws))], np.int32)
+                else:
+                    tiles = H.nbn_fin_tiles([r["F"] for r in rws]) if phase == 6 else \
+                        H.nbn_tiles([(r["R"], r["F"]) for r in rws], phase)
                 if len(tiles):
                     plan.launches.append(Launch("nbn", (phase, k_), desc_tensor(rws, H.NBN_DTYPE), T(tiles),
                                                 len(tiles)))
@@ -1044,6 +1135,8 @@ class HipPopulationEngine(PopulationEngine):
             for pid, col, width in fcat[o][fcons[o][n.id]]:
                 kt = -(-width // H.BK)
                 ns = max(1, min(16, kt // H.SPLIT_KSTEPS)) if H.SPLIT_KSTEPS > 0 else 1
+                if binslice(o, pid, n.id) is not None:
+                    ns = 1                              # the factorised slice writes one fp32 partial (bin_fwd)
                 out.append((pid, col, width, ns, S))
                 S += ns
             return out, S
@@ -1065,6 +1158,7 @@ class HipPopulationEngine(PopulationEngine):
         # ---- forward ---------------------------------------------------------------------------
         for d in range(1, maxd + 1):
             fin_rows = []
+            bin_rows = []
             g_rows, g_dims = [], []
             p_rows, p_cnt = [], []
             bn_rows, bn_cnt, bn_cnt_st, bn_stat = [], [], [], []
@@ -1120,6 +1214,10 @@ class HipPopulationEngine(PopulationEngine):
                             wsb = torch.zeros(S * M * F, dtype=torch.float32, device=self.device)
                             plan.keep.append(wsb)
                             for pid, col, width, ns, sb in sl:
+                                if binslice(o, pid, n.id) is not None:
+                                    bin_rows.append(dict(bin_desc(o, binslice(o, pid, n.id), n.id, col, width),
+                                                         slab=wsb.data_ptr() + 4 * sb * M * F))
+                                    continue
                                 g_rows.append(dict(a=self._act_ptr(mem, o, pid, inputs), b=wptr_bf(lay.w[n.id]) + 2 * col,
                                                    out=out, bias=0, H=1, W=1, C=width, OH=1, OW=1, F=F, KH=1, KW=1,
                                                    SH=1, SW=1, M=M, N=F, K=width, act=0, flags=0, ldb=D,
@@ -1161,7 +1259,7 @@ class HipPopulationEngine(PopulationEngine):
                                            OH=a["oh"], OW=a["ow"], PH=a["ph"], PW=a["pw"], SH=a["sh"], SW=a["sw"]))
                         p_cnt.append(H.pool_units(B * math.prod(n.shape), a["c"]))
                     elif n.op == "bn" and a["last"] and n.id in nbn[o]:
-                        nbn_rows.append(nbn_row(o, n.id))
+                        nbn_rows.append(dict(nbn_row(o, n.id), _bin=n.id in binpair[o]))
                     elif n.op == "bn" and a["last"]:
                         bd = rec["bn"][n.id]
                         c = a["channels"]
@@ -1235,13 +1333,17 @@ class HipPopulationEngine(PopulationEngine):
                     else:
                         raise ValueError(f"organism {o}: no kernel for op {n.op!r}")
             add_chunked("ew", 0, ew_pre, H.EW_DTYPE, [H.ew_count(r) for r in ew_pre], 1)
+            # factorised genotype slices: E / C0 from the weights, then their partial (before the finalize)
+            add_bin(0, bin_rows)
+            add_bin(1, bin_rows)
             add_gemm(H.MODE_FWD, g_rows, g_dims, extra_fin=fin_rows)
             add_chunked("pool", 0, p_rows, H.POOL_DTYPE, p_cnt, H.POOL_ELEMS)
             add_convpool(cp_rows, False)
             if train:
                 add_gchain([r for r in gc_rows if r["_bn"]], H.GC_FSTAT)
             add_gchain(gc_rows, H.GC_FAPPLY)
-            add_nbn(nbn_rows, 2)
+            add_nbn([r for r in nbn_rows if not r.get("_bin")], 2)
+            add_nbn([r for r in nbn_rows if r.get("_bin")], 2, stats_only=True)
             if bn_rows:
                 if train:
                     need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)
@@ -1383,6 +1485,14 @@ class HipPopulationEngine(PopulationEngine):
             cpw_rows = []
             gcb_rows = []
             nbnb_rows, nbnf_rows = [], []
+            bw_bin, bin_need = [], []           # factorised genotype slices of this depth (bnbn.hip)
+
+            def bin_ws(n64, need=bin_need):
+                """Reserve n64 int64 words of this depth's zeroed factorised-slice workspace (one memset launch);
+                returns a deferred address: the workspace is allocated once the depth's sizes are known."""
+                off = sum(need)
+                need.append(-(-n64 // 32) * 32 + 32)
+                return _Deferred(off)
             tasks = {s: [] for s in STAGES}     # stage -> [(o, owner|None, make_row(acc), count)]
             ew_bpre = []                        # non-last-axis BN: dy -> channels-last dyt
             for o, lay in org_iter():
@@ -1441,6 +1551,28 @@ class HipPopulationEngine(PopulationEngine):
                             D = C
                             sl, _ = concat_slices(o, n, F)
                             for q, (pid, col, width, ns, sb) in enumerate(sl):
+                                bpid = binslice(o, pid, n.id)
+                                if bpid is not None:
+                                    # factorised genotype slice: H = dZ^T g and cs = column sums of dZ by one
+                                    # WGRAD launch (Q40, plan-private zeroed buffers), then bin_s (the BN / Dense
+                                    # backward sums for nbn phase 6) and bin_wg (dW, Adam) after this depth's WGRADs
+                                    Lg = ir.genotype_size
+                                    hq = bin_ws(F * Lg + F)                 # Q40 H [F][L], then cs [F]
+                                    csq = hq + 8 * F * Lg
+                                    wg_rows.append(dict(a=dz, b=inputs[o]["g"], out=hq, bias=csq, aux=yv, act=act,
+                                                        H=Hh, W=1, C=Lg, OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=F,
+                                                        N=Lg, K=M, flags=(H.GF_VEC_A if F % 8 == 0 else 0),
+                                                        _nonarrow=1, _noadam=1))
+                                    wg_dims.append((F, Lg, M))
+                                    nbnsum_ext(o, bpid, 1, width)          # NbnDesc + part, one m slot
+                                    bw_bin.append(dict(bin_desc(o, bpid, n.id, col, width), Hm=hq, cs=csq,
+                                                       part=nbnsum_rows[o][bpid]["part"],
+                                                       dw=gptr(lay.w[n.id] + col), dbias=dbias if q == 0 else 0,
+                                                       adam=adam_ctx))
+                                    if adam_ctx:
+                                        plan.adam_regions.append(((gptr(lay.w[n.id] + col) - self.g.data_ptr()) // 8,
+                                                                  F, width, D))
+                                    continue
                                 wg_rows.append(dict(a=dz, b=self._act_ptr(mem, o, pid, inputs), out=gptr(lay.w[n.id] + col),
                                                     bias=dbias if q == 0 else 0, aux=yv, act=act, H=Hh, W=1, C=width,
                                                     OH=OH, OW=1, F=F, KH=1, KW=1, SH=1, SW=1, M=F, N=width, K=M,
@@ -1635,8 +1767,24 @@ class HipPopulationEngine(PopulationEngine):
             # bf16 weights the layer's DGRAD reads
             if adam_ctx:
                 for r in wg_rows:
-                    r["adam"] = adam_ctx
+                    if not r.get("_noadam"):
+                        r["adam"] = adam_ctx
+            if bin_need:
+                wsz = torch.empty(sum(bin_need) + 64, dtype=torch.int64, device=self.device)
+                plan.keep.append(wsz)
+                base_ = wsz.data_ptr()
+                for r in wg_rows:
+                    for k_ in ("out", "bias"):
+                        if isinstance(r.get(k_), _Deferred):
+                            r[k_] = r[k_].resolve(base_)
+                for r in bw_bin:
+                    for k_ in ("Hm", "cs"):
+                        r[k_] = r[k_].resolve(base_)
+                plan.launches.append(Launch("memset", (base_, 2 * wsz.numel()), None, None, 0))
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
+            # (bin_s reads the bf16 weights before bin_wg's Adam step rewrites them)
+            add_bin(3, bw_bin)
+            add_bin(4, bw_bin)
         # descriptor / tile tables are uploaded from pageable host memory: fence them before a launch can
         # read them.  Plans are built once per generation, so this costs nothing on the training hot path.
         tables.flush(plan.keep)
@@ -1683,6 +1831,8 @@ class HipPopulationEngine(PopulationEngine):
         metrics = torch.zeros(P, 4, dtype=torch.int64, device=dev)      # Q32 fixed point (aux.hip loss_kernel)
 
         self.diverged.zero_()                       # (flags of this fit only)
+        # binary genotype batches enable the factorised genotype-slice path (bnbn.hip); checked on the host data
+        self._g_binary = _is_binary(data.train_g)
         t_plan = time.perf_counter()
         mem = self._alloc_buffers(B, with_grads=True)
         self.timings["alloc_s"] = time.perf_counter() - t_plan
@@ -1914,6 +2064,7 @@ class HipPopulationEngine(PopulationEngine):
         metrics = torch.zeros(self.num_organisms, 4, dtype=torch.int64, device=dev)
         mem = self._alloc_buffers(B, with_grads=True)
         inputs = [{"X": xb.data_ptr(), "g": gb.data_ptr()} for _ in range(self.num_organisms)]
+        self._g_binary = _is_binary(g)
         plan = self._build_plan("train", B, mem, inputs, yb.data_ptr(), [gb.data_ptr()] * self.num_organisms, metrics)
         s = H.stream_handle()
         self.g.zero_()

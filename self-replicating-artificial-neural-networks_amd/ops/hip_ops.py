@@ -37,6 +37,9 @@ EW_ELEMS = 2048        # ew.hip: destination elements per block
 SPLITFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "bias", "M", "N", "S", "act", "flags"]])
 SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kernel
 WGFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "adam", "M", "N", "C", "Cp", "S", "ldo", "flags"]])
+BIN_DTYPE = np.dtype([(f, _I) for f in ["g", "w", "bias", "gamma", "beta", "mean", "invstd", "act", "flags", "wc", "ldw",
+                                        "Nc", "L", "F", "B", "E", "C0", "slab", "Hm", "cs", "part", "dw", "dbias",
+                                        "adam"]])
 WGFIN_ELEMS = 64       # aux.hip: outputs per block of the split WGRAD finalize kernel
 CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy", "dw", "dbias", "B", "H", "W", "F",
                                              "KH", "KW", "SH", "SW", "OH", "OW", "PH", "PW", "PSH", "PSW", "POH",
@@ -419,7 +422,8 @@ def check_layouts():
                      ("TransDesc", TRANS_DTYPE), ("ImcolDesc", IMCOL_DTYPE), ("SplitFinDesc", SPLITFIN_DTYPE),
                      ("WgFinDesc", WGFIN_DTYPE),
                      ("ConvPoolDesc", CONVPOOL_DTYPE), ("GChainDesc", GCHAIN_DTYPE),
-                     ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE), ("AdamCtx", ADAM_CTX_DTYPE)]:
+                     ("RepBitsDesc", REPBITS_DTYPE), ("NbnDesc", NBN_DTYPE), ("AdamCtx", ADAM_CTX_DTYPE),
+                     ("BinDesc", BIN_DTYPE)]:
         if sizes[name] != dt.itemsize:
             raise RuntimeError(f"descriptor layout mismatch for {name}: C++ {sizes[name]} vs numpy {dt.itemsize}")
 
@@ -680,6 +684,8 @@ def conv_wgrad_splits(nchunks: int, wave_mfmas_per_chunk: int, tiles: int = 1, s
 
 
 NARROW_ROWS, NARROW_WROWS = 256, 1024   # gemm3.hip narrow (K <= 4) kernels: rows per block
+# rows per block of a statistics-only narrow FWD (GF_BNSTAT | GF_NOSTORE, super-row kernel; a multiple of 8)
+NARROW_NOSTORE_ROWS = int(_os.environ.get("SERANN_NARROW_NOSTORE_ROWS", "2048"))
 
 # A/B switches for measurements and fault isolation (all paths are on by default)
 _OFF = set(filter(None, _os.environ.get("SERANN_GEMM3_OFF", "").split(",")))   # conv_fwd,conv_wgrad,narrow,sk
@@ -803,9 +809,13 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     for v in sorted(groups):
         items = groups[v]
         if (mode == MODE_FWD and 6000 <= v < 7000) or (mode == MODE_WGRAD and 4000000 <= v < 5000000):
-            per = NARROW_ROWS if mode == MODE_FWD else NARROW_WROWS
             tl = []
             for p, (r, (M, N, K)) in enumerate(items):
+                per = NARROW_ROWS if mode == MODE_FWD else NARROW_WROWS
+                if mode == MODE_FWD and v % 1000 >= 200 and int(r.get("flags", 0)) & GF_NOSTORE:
+                    # statistics-only super-row pass: longer row blocks (the kernel reads them from kper)
+                    per = NARROW_NOSTORE_ROWS
+                    r["kper"] = per
                 nrows = M if mode == MODE_FWD else K
                 nb = -(-nrows // per)
                 tl.append(np.stack([np.full(nb, p), np.arange(nb), np.zeros(nb, int), np.zeros(nb, int)], 1))

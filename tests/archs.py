@@ -123,6 +123,14 @@ ARCHS = {
         "g_layer = BatchNormalization()(g_layer)\n\n"
         "con = concatenate([Reshape((1, -1))(X_layer), Reshape((1, -1))(g_layer)])\n\n"
         "con = Dense(units=48, activation='relu')(con)\n\nloss_balance = 0.5"),
+    # the binary-genotype factorisation (csrc/hip/bnbn.hip) with the genotype slice FIRST in the concat (it carries
+    # the merged Dense's bias gradient) and a linear raw-genotype Dense
+    "bnbn_g_first_linear": (
+        "X_layer = Conv2D(filters=8, kernel_size=3, strides=2)(X_layer)\n\n"
+        "g_layer = Dense(units=32)(g_layer)\n"
+        "g_layer = BatchNormalization()(g_layer)\n\n"
+        "con = concatenate([Reshape((1, -1))(g_layer), Reshape((1, -1))(X_layer)])\n\n"
+        "con = Dense(units=40, activation='sigmoid')(con)\n\nloss_balance = 0.35"),
     "nbn_wide_linear": (
         "X_layer = Dense(units=8)(X_layer)\n"
         "X_layer = BatchNormalization()(X_layer)\n\n"

@@ -490,6 +490,7 @@ def test_nbn_sums_in_dgrad_match_phases_4_5(name, monkeypatch):
     production batch."""
     from serann.engine import hip_engine as he
     from serann.ops import hip_ops as H
+    monkeypatch.setattr(he, "BINARY_NBN", False)        # (the GEMM path of the pair: GF_NBNSUM)
     ir = interpret(ARCHS[name])
     params = init_params(ir, 3)
     x, g, y = _batch(750, seed=2)
@@ -711,3 +712,60 @@ def test_tiled_n_tile_groups_are_bitwise_neutral(name, monkeypatch):
     (g1, l1, m1, n1), (g3, l3, m3, n3) = out
     assert n1 > 0 and n3 == n1
     assert torch.equal(g1, g3) and np.array_equal(l1, l3) and np.array_equal(m1, m3)
+
+
+@pytest.mark.parametrize("name", ["narrow_bn_ancestor", "nbn_sum_acts", "bnbn_g_first_linear"])
+def test_binary_genotype_factorisation_matches_the_gemm_path(name, monkeypatch):
+    """The factorised genotype slice (csrc/hip/bnbn.hip: bin_prep / bin_fwd / the H WGRAD / bin_s / bin_wg; the BN
+    output never written) against the GEMM path of the same pair (K-slice FWD, GF_NBNSUM DGRAD, slice WGRAD) on one
+    production-batch step: logits and every gradient at least as close to the fp32 oracle (1.25x + 1 % slack)."""
+    from serann.engine import hip_engine as he
+    ir = interpret(ARCHS[name])
+    params = init_params(ir, 4)
+    x, g, y = _batch(750, seed=3)
+    fact = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gf, mf = fact.debug_train_step(x, g, y)
+    assert sorted({la.arg for la in fact._debug_plan.launches if la.kind == "bin"}) == [0, 1, 3, 4]
+    lf = fact.debug_logits()[0]
+    monkeypatch.setattr(he, "BINARY_NBN", False)
+    plain = he.HipPopulationEngine([ir], [0], device="cuda", params=[params])
+    gp, mp = plain.debug_train_step(x, g, y)
+    assert not any(la.kind == "bin" for la in plain._debug_plan.launches)
+    lp = plain.debug_logits()[0]
+    ref_logits, ref = _oracle(ir, params, x, g, y)
+    assert _rel(lf, ref_logits) < 1.25 * _rel(lp, ref_logits) + 1e-3, (_rel(lf, ref_logits), _rel(lp, ref_logits))
+    a, b = fact.export_arena(0, gf), plain.export_arena(0, gp)
+    gmax = max(float(np.abs(v).max()) for d in ref.values() for v in d.values())
+    for nid in ref:
+        for k in ref[nid]:
+            r = np.asarray(ref[nid][k], np.float64)
+            ef, eu = np.linalg.norm(a[nid][k] - r), np.linalg.norm(b[nid][k] - r)
+            floor = 1e-3 * gmax * np.sqrt(r.size)
+            assert ef < 1.25 * eu + 0.01 * np.linalg.norm(r) + floor, (name, nid, k, ef, eu, np.linalg.norm(r))
+    assert np.array_equal(mf[:, 3], mp[:, 3])
+    fact.close()
+    plain.close()
+
+
+def test_binary_genotype_factorisation_fit_matches_the_gemm_path(monkeypatch):
+    """Three-epoch fits (graph replay, 4 stream groups, fused Adam in bin_wg with 16-bit moments) of binary-path
+    organisms against the GEMM path: validation accuracies within 0.03 once converged, and the factorised fit is
+    bitwise reproducible."""
+    from serann.data.datasets import get_serann_data, synthetic_encodings, synthetic_mnist
+    from serann.engine import hip_engine as he
+    from serann.engine.base import TrainConfig
+    data = get_serann_data(synthetic_encodings(), synthetic_mnist(n_train=6000, n_test=300, seed=21),
+                           n_train=6000, n_test=300)
+    names = ["narrow_bn_ancestor", "nbn_sum_acts", "bnbn_g_first_linear", "conv_pool_dense"]
+    irs = [interpret(ARCHS[n]) for n in names]
+    cfg = TrainConfig(epochs=3, batch_size=250, val_every_epoch=False)
+    out = []
+    for binary in (True, True, False):
+        monkeypatch.setattr(he, "BINARY_NBN", binary)
+        eng = he.HipPopulationEngine(irs, list(range(len(irs))), device="cuda", cfg=cfg)
+        res = eng.fit(data, cfg)
+        out.append((eng.p.cpu(), res.val_acc))
+        del eng
+    (p1, a1), (p2, a2), (_, a3) = out
+    assert torch.equal(p1, p2) and np.array_equal(a1, a2)
+    assert np.all(np.abs(a1 - a3) <= 0.03), (a1, a3)
