@@ -16,12 +16,14 @@
 // ones at position p.  The slice's GEMMs (FWD over K = L F = 7500, DGRAD to [B][7500], WGRAD over B rows) become
 // K = L GEMMs and elementwise passes, and y is never written: the same function of the weights and the genotype
 // batch (Y0 / Y1 are the bf16 values the unfactorised GEMMs read), summed in another order.
-//   bin_prep  per (problem, n): Y0, D (LDS), E[.][n], C0[n]               (reads W once)
-//   bin_fwd   per (problem, 32 rows): the slice's fp32 partial of out into its split-K workspace slot
+//   bin_prep  per (problem, n): Y0, D; the row's W staged through LDS in whole positions; E[.][n], C0[n]
+//   bin_fwd   per (problem, 32 rows): the slice's fp32 partial of out into its split-K workspace slot; each thread
+//             holds its column's 32 accumulators and reads E[p][n] once per position
 //   (H and cs: one Dense WGRAD launch of the existing gemm3 kernel, dW = dZ^T g with dZ's column sums as the "bias
 //    gradient", in Q40 fixed point into the step's zeroed workspace -- the planner adds it, K = B rows)
-//   bin_s     per (problem, position): N1, the 8 sums into NbnDesc::part slot 0 (nbn phase 6 finishes them)
-//   bin_wg    per (problem, n): dW of the slice -> Q40 store, or Keras-Adam applied in place (sole writer)
+//   bin_sw    per (problem, 64 or 256 slice columns j = pF + f): one pass down the columns (4 waves over the Nc rows) reads each
+//             weight once for S1 / St and, as the element's sole writer, stores its Q40 gradient or applies
+//             Keras-Adam in place; then N1 and the 8 sums into NbnDesc::part slot 0 (nbn phase 6 finishes them)
 // Every sum runs in a fixed order (no atomics besides the consumer-bias fx_add): bitwise reproducible.
 #include "common.h"
 #include "serann_hip.h"
@@ -72,7 +74,8 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
 
 }  // namespace
 
-// tiles: (problem, n)
+// tiles: (problem, n).  Four lanes per position (f = q, q + 4, ...), 64 positions per pass; the lanes' partial E
+// meet in a fixed-order pair exchange
 __global__ __launch_bounds__(256) void bin_prep_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
     __shared__ float sY0[256], sD[256], red[4];
     const int2 td = tiles[blockIdx.x];
@@ -86,16 +89,29 @@ __global__ __launch_bounds__(256) void bin_prep_kernel(const BinDesc* __restrict
     }
     __syncthreads();
     const bf16_t* __restrict__ Wr = reinterpret_cast<const bf16_t*>(d.wc) + (int64_t)n * d.ldw;
+    float* __restrict__ E = reinterpret_cast<float*>(d.E);
+    const int q = t & 3, pl = t >> 2;
     float c0 = 0.f;
-    if (t < L) {
+    for (int p0 = 0; p0 < L; p0 += 64) {
+        const int p = p0 + pl;
         float e = 0.f;
-        const bf16_t* wp = Wr + t * F;
-        for (int f = 0; f < F; ++f) {
-            const float wv = bf2f(wp[f]);
-            e += sD[f] * wv;
-            c0 += sY0[f] * wv;
+        if (p < L) {
+            const bf16_t* __restrict__ wp = Wr + p * F;
+            for (int f0 = q; f0 < F; f0 += 32) {         // eight loads in flight per lane
+                float wv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) wv[k] = f0 + 4 * k < F ? bf2f(wp[f0 + 4 * k]) : 0.f;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int f = min(f0 + 4 * k, F - 1);
+                    e = fmaf(sD[f], wv[k], e);
+                    c0 = fmaf(sY0[f], wv[k], c0);
+                }
+            }
         }
-        reinterpret_cast<float*>(d.E)[(int64_t)t * Nc + n] = e;
+        e += __shfl_xor(e, 1, 64);
+        e += __shfl_xor(e, 2, 64);
+        if (q == 0 && p < L) E[(int64_t)p * Nc + n] = e;
     }
     c0 = block_sum256(c0, red);
     if (t == 0) reinterpret_cast<float*>(d.C0)[n] = c0;
@@ -104,114 +120,229 @@ __global__ __launch_bounds__(256) void bin_prep_kernel(const BinDesc* __restrict
 // tiles: (problem, first row / 32)
 constexpr int BIN_ROWS = 32;
 __global__ __launch_bounds__(256) void bin_fwd_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
-    __shared__ float sg[BIN_ROWS * 256];
+    __shared__ float sg[256 * BIN_ROWS];             // g transposed: [position][row]
     const int2 td = tiles[blockIdx.x];
     const BinDesc& d = descs[td.x];
     const int L = (int)d.L, Nc = (int)d.Nc, M = (int)d.B;
     const int m0 = td.y * BIN_ROWS, nr = min(BIN_ROWS, M - m0);
-    const bf16_t* __restrict__ g = reinterpret_cast<const bf16_t*>(d.g);
-    for (int i = threadIdx.x; i < nr * L; i += 256) sg[i] = bf2f(g[(int64_t)m0 * L + i]);
+    const bf16_t* __restrict__ g = reinterpret_cast<const bf16_t*>(d.g) + (int64_t)m0 * L;
+    for (int i = threadIdx.x; i < BIN_ROWS * L; i += 256) {
+        const int r = i / L, p = i - r * L;
+        sg[p * BIN_ROWS + r] = r < nr ? bf2f(g[i]) : 0.f;
+    }
     __syncthreads();
-    const int n = threadIdx.x;
-    if (n >= Nc) return;
     const float* __restrict__ E = reinterpret_cast<const float*>(d.E);
-    const float c0 = reinterpret_cast<const float*>(d.C0)[n];
-    float* __restrict__ slab = reinterpret_cast<float*>(d.slab);
-    for (int r = 0; r < nr; ++r) {
-        float acc = c0;
-        for (int p = 0; p < L; ++p) acc += sg[r * L + p] * E[(int64_t)p * Nc + n];
-        slab[(int64_t)(m0 + r) * Nc + n] = acc;
+    float* __restrict__ slab = reinterpret_cast<float*>(d.slab) + (int64_t)m0 * Nc;
+    for (int n = threadIdx.x; n < Nc; n += 256) {
+        const float c0 = reinterpret_cast<const float*>(d.C0)[n];
+        float acc[BIN_ROWS];
+#pragma unroll
+        for (int r = 0; r < BIN_ROWS; ++r) acc[r] = c0;
+        for (int p = 0; p < L; ++p) {
+            const float e = E[(int64_t)p * Nc + n];
+            const float4* gp = reinterpret_cast<const float4*>(sg + p * BIN_ROWS);
+#pragma unroll
+            for (int q = 0; q < BIN_ROWS / 4; ++q) {
+                const float4 gv = gp[q];
+                acc[4 * q + 0] += gv.x * e;
+                acc[4 * q + 1] += gv.y * e;
+                acc[4 * q + 2] += gv.z * e;
+                acc[4 * q + 3] += gv.w * e;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < BIN_ROWS; ++r)
+            if (r < nr) slab[(int64_t)r * Nc + n] = acc[r];
     }
 }
 
-// tiles: (problem, position)
-__global__ __launch_bounds__(256) void bin_s_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
-    __shared__ float red[4];
-    const int2 td = tiles[blockIdx.x];
-    const BinDesc& d = descs[td.x];
-    const int F = (int)d.F, Nc = (int)d.Nc, L = (int)d.L, M = (int)d.B, p = td.y;
-    const int f = threadIdx.x;
-    // N1[p]: the ones at position p over the batch (fixed-order block sum)
-    const bf16_t* __restrict__ g = reinterpret_cast<const bf16_t*>(d.g);
-    float c = 0.f;
-    for (int m = threadIdx.x; m < M; m += 256) c += bf2f(g[(int64_t)m * L + p]);
-    const float N1 = block_sum256(c, red), N0 = (float)M - N1;
-    const long long* __restrict__ Hq = reinterpret_cast<const long long*>(d.Hm);   // Q40 [Nc][L]
-    const long long* __restrict__ csq = reinterpret_cast<const long long*>(d.cs);  // Q40 [Nc]
-    if (p == 0 && d.dbias && f < Nc) fx_add(reinterpret_cast<long long*>(d.dbias) + f, fx_f(csq[f]));
-    if (f >= F) return;
-    const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(d.wc) + p * F + f;
-    float s1 = 0.f, st = 0.f;
-    for (int n = 0; n < Nc; ++n) {
-        const float wv = bf2f(W[(int64_t)n * d.ldw]);
-        s1 += fx_f(Hq[(int64_t)n * L + p]) * wv;
-        st += fx_f(csq[n]) * wv;
+// tiles: (problem, 64 V-column block of the slice): lane -> columns j = pF + f .. + V - 1, wave -> rows n = wave,
+// wave + 4, ...  V = 4 (BIN_VEC4: 16-B fp32 / 8-B 16-bit accesses) when the slice's columns, row stride and arena
+// offset are multiples of 4 and F >= 4 (a lane's columns span at most two positions), else V = 1.
+// MM: Adam moment storage (common.h).  Explicit fmaf: the store and the fused-Adam branches must round alike (the
+// arena pass and the in-place update see the same gradient)
+constexpr int BIN_NL = 4, BIN_UNROLL = 2, BIN_VEC4 = 4;
+__device__ __forceinline__ float bin_grad(float Y0, float Dd, float c, float h) { return fmaf(Dd, h, Y0 * c); }
+
+template <int V> __device__ __forceinline__ void ldv_bf(const bf16_t* p, float* x) {
+    if constexpr (V == 4) {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        x[0] = __uint_as_float(u.x << 16); x[1] = __uint_as_float(u.x & 0xffff0000u);
+        x[2] = __uint_as_float(u.y << 16); x[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+        x[0] = bf2f(p[0]);
     }
-    const BinUnit u = bin_unit(d, f);
-    const float s0 = st - s1;
-    // the eight sums of gemm3.hip's GF_NBNSUM epilogue over the column's B rows (x = g in {0, 1}):
-    //   [0] dy  [1] dy xhat  [2] a dy  [3] a xhat  [4] a  [5] a x dy  [6] a x xhat  [7] a x
-    float* __restrict__ out = reinterpret_cast<float*>(d.part) + ((int64_t)p * F + f) * NBN_NSUM;
-    const float4 lo = make_float4(st, u.xh0 * s0 + u.xh1 * s1, u.a0 * s0 + u.a1 * s1,
-                                  u.a0 * u.xh0 * N0 + u.a1 * u.xh1 * N1);
-    const float4 hi = make_float4(u.a0 * N0 + u.a1 * N1, u.a1 * s1, u.a1 * u.xh1 * N1, u.a1 * N1);
-    *reinterpret_cast<float4*>(out) = lo;
-    *reinterpret_cast<float4*>(out + 4) = hi;
+}
+template <int V> __device__ __forceinline__ void ldv_f(const float* p, float* x) {
+    if constexpr (V == 4) { const float4 u = *reinterpret_cast<const float4*>(p); x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w; }
+    else x[0] = p[0];
+}
+template <int MM, int V> __device__ __forceinline__ void ldv_m(const void* b, int64_t e, float* x, bool second) {
+    if constexpr (V == 4) {
+        const float4 u = second ? v_ld4<MM>(b, e) : m_ld4<MM>(b, e);
+        x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
+    } else {
+        x[0] = second ? v_ld<MM>(b, e) : m_ld<MM>(b, e);
+    }
 }
 
-// tiles: (problem, n).  MM: Adam moment storage (common.h)
-template <int MM>
-__device__ __forceinline__ void bin_wg_row(const BinDesc& d, int n, const float* sY0, const float* sD) {
-    const int L = (int)d.L, F = (int)d.F, W = L * F;
-    const float csn = fx_f(reinterpret_cast<const long long*>(d.cs)[n]);
-    const long long* __restrict__ Hq = reinterpret_cast<const long long*>(d.Hm) + (int64_t)n * L;   // Q40 [Nc][L]
-    long long* __restrict__ out = reinterpret_cast<long long*>(d.dw) + (int64_t)n * d.ldw;
+template <int MM, int V>
+__device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nl, const int* pc, const float* Y0,
+                                            const float* Dd, float* s1, float* st) {
+    const int Nc = (int)d.Nc, L = (int)d.L;
+    const int64_t ldw = d.ldw;
+    const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(d.wc) + j;
+    const long long* __restrict__ Hq = reinterpret_cast<const long long*>(d.Hm);       // Q40 [Nc][L]
+    const long long* __restrict__ csq = reinterpret_cast<const long long*>(d.cs);      // Q40 [Nc]
+    long long* __restrict__ out = reinterpret_cast<long long*>(d.dw) + j;
+    // a lane's columns lie in positions pc[0] and pc[0] + 1 (F >= V)
+    const int pa = pc[0], pb = min(pc[0] + 1, L - 1);
     if (!d.adam) {
-        for (int j = threadIdx.x; j < W; j += 256) {
-            const int p = j / F, f = j - p * F;
-            out[j] = fx_q(sY0[f] * csn + sD[f] * fx_f(Hq[p]));
+        for (int n = nl; n < Nc; n += BIN_NL) {
+            const float ha = fx_f(Hq[(int64_t)n * L + pa]), hb = fx_f(Hq[(int64_t)n * L + pb]), c = fx_f(csq[n]);
+            float w[V];
+            ldv_bf<V>(W + n * ldw, w);
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const float h = pc[k] == pa ? ha : hb;
+                s1[k] = fmaf(h, w[k], s1[k]);
+                st[k] = fmaf(c, w[k], st[k]);
+                out[n * ldw + k] = fx_q(bin_grad(Y0[k], Dd[k], c, h));
+            }
         }
         return;
     }
     const AdamCtx ac = *reinterpret_cast<const AdamCtx*>(d.adam);
     const int64_t e0 = out - reinterpret_cast<const long long*>(ac.g);
-    float* __restrict__ P = reinterpret_cast<float*>(ac.p);
-    void* __restrict__ Mo = reinterpret_cast<void*>(ac.m);
-    void* __restrict__ Vo = reinterpret_cast<void*>(ac.v);
-    bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf);
+    float* __restrict__ P = reinterpret_cast<float*>(ac.p) + e0;
+    bf16_t* __restrict__ Pb = reinterpret_cast<bf16_t*>(ac.pbf) + e0;
     const float lr_t = *reinterpret_cast<const float*>(ac.lr_t);
     const int64_t* __restrict__ org_off = reinterpret_cast<const int64_t*>(ac.org_off);
     int* __restrict__ diverged = reinterpret_cast<int*>(ac.diverged);
     const int norg = (int)ac.norg;
-    for (int j = threadIdx.x; j < W; j += 256) {
-        const int p = j / F, f = j - p * F;
-        const float gq = fx_f(fx_q(sY0[f] * csn + sD[f] * fx_f(Hq[p])));   // as the Q40 arena would hold it
-        const int64_t e = e0 + j;
-        if (SERANN_DIVERGE_CHECK && org_off != nullptr && fabsf(gq) > FX_DIVERGE) flag_diverged(org_off, diverged, norg, e);
-        float p_ = P[e], m_ = m_ld<MM>(Mo, e), v_ = v_ld<MM>(Vo, e);
-        adam_elem(p_, m_, v_, gq, lr_t, ac.b1, ac.b2, ac.eps);
-        P[e] = p_;
-        m_st<MM>(Mo, e, m_);
-        v_st<MM>(Vo, e, v_);
-        Pb[e] = f2bf(p_);
+    const float b1 = ac.b1, b2 = ac.b2, eps = ac.eps;
+    void* __restrict__ Mo = reinterpret_cast<void*>(ac.m);
+    void* __restrict__ Vo = reinterpret_cast<void*>(ac.v);
+    for (int n0 = nl; n0 < Nc; n0 += BIN_NL * BIN_UNROLL) {
+        float w[BIN_UNROLL][V], p_[BIN_UNROLL][V], m_[BIN_UNROLL][V], v_[BIN_UNROLL][V];
+        float ha[BIN_UNROLL], hb[BIN_UNROLL], c[BIN_UNROLL];
+#pragma unroll
+        for (int u = 0; u < BIN_UNROLL; ++u) {                 // all loads of the group first
+            const int n = min(n0 + u * BIN_NL, Nc - 1);
+            const int64_t o = n * ldw;
+            ldv_bf<V>(W + o, w[u]);
+            ldv_f<V>(P + o, p_[u]);
+            ldv_m<MM, V>(Mo, e0 + o, m_[u], false);
+            ldv_m<MM, V>(Vo, e0 + o, v_[u], true);
+            ha[u] = fx_f(Hq[(int64_t)n * L + pa]);
+            hb[u] = fx_f(Hq[(int64_t)n * L + pb]);
+            c[u] = fx_f(csq[n]);
+        }
+#pragma unroll
+        for (int u = 0; u < BIN_UNROLL; ++u) {
+            if (n0 + u * BIN_NL >= Nc) break;
+            const int64_t o = (int64_t)(n0 + u * BIN_NL) * ldw;
+#pragma unroll
+            for (int k = 0; k < V; ++k) {
+                const float h = pc[k] == pa ? ha[u] : hb[u];
+                s1[k] = fmaf(h, w[u][k], s1[k]);
+                st[k] = fmaf(c[u], w[u][k], st[k]);
+                const float gq = fx_f(fx_q(bin_grad(Y0[k], Dd[k], c[u], h)));   // as the Q40 arena would hold it
+                if (SERANN_DIVERGE_CHECK && org_off != nullptr && fabsf(gq) > FX_DIVERGE)
+                    flag_diverged(org_off, diverged, norg, e0 + o + k);
+                adam_elem(p_[u][k], m_[u][k], v_[u][k], gq, lr_t, b1, b2, eps);
+            }
+            if constexpr (V == 4) {
+                *reinterpret_cast<float4*>(P + o) = make_float4(p_[u][0], p_[u][1], p_[u][2], p_[u][3]);
+                m_st4<MM>(Mo, e0 + o, make_float4(m_[u][0], m_[u][1], m_[u][2], m_[u][3]));
+                v_st4<MM>(Vo, e0 + o, make_float4(v_[u][0], v_[u][1], v_[u][2], v_[u][3]));
+                *reinterpret_cast<uint2*>(Pb + o) = make_uint2(f2bf2(p_[u][0], p_[u][1]), f2bf2(p_[u][2], p_[u][3]));
+            } else {
+                P[o] = p_[u][0];
+                m_st<MM>(Mo, e0 + o, m_[u][0]);
+                v_st<MM>(Vo, e0 + o, v_[u][0]);
+                Pb[o] = f2bf(p_[u][0]);
+            }
+        }
     }
 }
 
-__global__ __launch_bounds__(256) void bin_wg_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
-    __shared__ float sY0[256], sD[256];
-    const int2 td = tiles[blockIdx.x];
-    const BinDesc& d = descs[td.x];
-    const int t = threadIdx.x;
-    if (t < (int)d.F) {
-        const BinUnit u = bin_unit(d, t);
-        sY0[t] = u.Y0;
-        sD[t] = u.D;
+template <int V>
+__device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb) {
+    constexpr int COLS = 64 * V;
+    __shared__ float red[256], sN1[256], sS1[BIN_NL][COLS], sSt[BIN_NL][COLS];
+    const int F = (int)d.F, Nc = (int)d.Nc, L = (int)d.L, M = (int)d.B, W = L * F;
+    const int t = threadIdx.x, lane = t & 63, nl = t >> 6;
+    const int j0 = jb * COLS, j = j0 + lane * V;
+    if (jb == 0 && d.dbias) {                         // the consumer's bias gradient: cs, once per problem
+        const long long* __restrict__ csq = reinterpret_cast<const long long*>(d.cs);
+        for (int n = t; n < Nc; n += 256) fx_add(reinterpret_cast<long long*>(d.dbias) + n, fx_f(csq[n]));
+    }
+    // N1 of the block's positions [pl, pl + np): thread (mi, pi) sums rows mi, mi + nm, ... of position pl + pi
+    const int pl = j0 / F, np = min(L - 1, (j0 + COLS - 1) / F) - pl + 1, nm = 256 / np;
+    {
+        const bf16_t* __restrict__ g = reinterpret_cast<const bf16_t*>(d.g) + pl;
+        const int pi = t % np, mi = t / np;
+        float c = 0.f;
+        if (mi < nm)
+            for (int m = mi; m < M; m += nm) c += bf2f(g[(int64_t)m * L + pi]);
+        red[t] = c;
+        __syncthreads();
+        if (t < np) {
+            float s = 0.f;
+            for (int k = 0; k < nm; ++k) s += red[k * np + t];
+            sN1[t] = s;
+        }
+    }
+    int pc[V];
+    float Y0[V], Dd[V], s1[V], st[V];
+    BinUnit u[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int jc = min(j + k, W - 1);
+        pc[k] = jc / F;
+        u[k] = bin_unit(d, jc - pc[k] * F);
+        Y0[k] = u[k].Y0;
+        Dd[k] = u[k].D;
+        s1[k] = st[k] = 0.f;
+    }
+    if (j < W) {
+        if (d.adam && reinterpret_cast<const AdamCtx*>(d.adam)->mode == MOM_16)
+            bin_sw_cols<MOM_16, V>(d, j, nl, pc, Y0, Dd, s1, st);
+        else
+            bin_sw_cols<MOM_F32, V>(d, j, nl, pc, Y0, Dd, s1, st);
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        sS1[nl][lane * V + k] = s1[k];
+        sSt[nl][lane * V + k] = st[k];
     }
     __syncthreads();
-    if (d.adam && reinterpret_cast<const AdamCtx*>(d.adam)->mode == MOM_16)
-        bin_wg_row<MOM_16>(d, td.y, sY0, sD);
+    if (nl != 0) return;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int c = lane * V + k;
+        if (j + k >= W) break;
+        const float S1 = ((sS1[0][c] + sS1[1][c]) + sS1[2][c]) + sS1[3][c];
+        const float St = ((sSt[0][c] + sSt[1][c]) + sSt[2][c]) + sSt[3][c];
+        const float N1 = sN1[pc[k] - pl], N0 = (float)M - N1, s0 = St - S1;
+        const BinUnit& q = u[k];
+        // the eight sums of gemm3.hip's GF_NBNSUM epilogue over the column's B rows (x = g in {0, 1}):
+        //   [0] dy  [1] dy xhat  [2] a dy  [3] a xhat  [4] a  [5] a x dy  [6] a x xhat  [7] a x
+        float* __restrict__ o = reinterpret_cast<float*>(d.part) + (int64_t)(j + k) * NBN_NSUM;
+        *reinterpret_cast<float4*>(o) = make_float4(St, q.xh0 * s0 + q.xh1 * S1, q.a0 * s0 + q.a1 * S1,
+                                                    q.a0 * q.xh0 * N0 + q.a1 * q.xh1 * N1);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(q.a0 * N0 + q.a1 * N1, q.a1 * S1, q.a1 * q.xh1 * N1, q.a1 * N1);
+    }
+}
+
+__global__ __launch_bounds__(256) void bin_sw_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
+    const int2 td = tiles[blockIdx.x];
+    const BinDesc& d = descs[td.x];
+    if (d.flags & BIN_VEC4)
+        bin_sw_block<4>(d, td.y);
     else
-        bin_wg_row<MOM_F32>(d, td.y, sY0, sD);
+        bin_sw_block<1>(d, td.y);
 }
 
 void launch_bin(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
@@ -223,8 +354,7 @@ void launch_bin(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint6
     switch (phase) {
         case 0: hipLaunchKernelGGL(bin_prep_kernel, grid, block, 0, s, dp, tp); break;
         case 1: hipLaunchKernelGGL(bin_fwd_kernel, grid, block, 0, s, dp, tp); break;
-        case 3: hipLaunchKernelGGL(bin_s_kernel, grid, block, 0, s, dp, tp); break;
-        case 4: hipLaunchKernelGGL(bin_wg_kernel, grid, block, 0, s, dp, tp); break;
+        case 3: hipLaunchKernelGGL(bin_sw_kernel, grid, block, 0, s, dp, tp); break;
         default: throw std::runtime_error("bin: unknown phase " + std::to_string(phase));
     }
     SERANN_CHECK(hipGetLastError());

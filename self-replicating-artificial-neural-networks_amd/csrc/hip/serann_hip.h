@@ -185,7 +185,7 @@ struct LossDesc {
 
 // Binary-genotype factorisation of a raw-genotype Dense -> BN pair's merged-Dense K slice (bnbn.hip).  g: raw genotype
 // bf16 [B][L] in {0, 1}; w / bias / act: the pair's Dense (K = 1); gamma / beta / mean / invstd: its BN (flags 1 gamma,
-// 2 beta); wc: the consumer's bf16 weights at the slice (W[n][col + j], row stride ldw), Nc units; E fp32 [L][Nc],
+// 2 beta, 4 BIN_VEC4: bin_sw's 4-column lanes); wc: the consumer's bf16 weights at the slice (W[n][col + j], row stride ldw), Nc units; E fp32 [L][Nc],
 // C0 fp32 [Nc]; slab: the slice's fp32 slot [B][Nc] of the consumer's split-K workspace; Hm, cs: Q40 H [Nc][L] and
 // column sums of dZ [Nc] (written by a gemm3 WGRAD launch); part: NbnDesc::part slot 0 [L F][8]; dw: the slice's Q40
 // gradient (row stride ldw); dbias: the consumer's Q40 bias gradient when the slice carries it; adam: AdamCtx (0: store)
@@ -194,5 +194,6 @@ struct BinDesc {
     int64_t wc, ldw, Nc, L, F, B;
     int64_t E, C0, slab, Hm, cs, part, dw, dbias, adam;
 };
+// phase 0 bin_prep (problem, n), 1 bin_fwd (problem, 32 rows), 3 bin_sw (problem, 64 slice columns)
 void launch_bin(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 

@@ -125,6 +125,7 @@ def gchain_triples(ir: OrganismIR) -> Dict[int, Tuple[int, int, Optional[int]]]:
 FUSE_NBN = os.environ.get("SERANN_FUSE_NBN", "1") != "0"
 # binary-genotype factorisation of raw-genotype Dense -> BN pairs read by a merged-Dense K slice (csrc/hip/bnbn.hip)
 BINARY_NBN = os.environ.get("SERANN_BINARY_NBN", "1") != "0"
+BIN_VEC4 = os.environ.get("SERANN_BIN_VEC4", "1") != "0"
 # fused pairs whose BN output feeds one LDS-tiled DGRAD: BN backward sums in that DGRAD's epilogue (nbn phase 6)
 NBN_SUM = os.environ.get("SERANN_NBNSUM", "1") != "0"
 
@@ -1056,10 +1057,8 @@ class HipPopulationEngine(PopulationEngine):
                 counts = [int(r["Nc"]) for r in rows]
             elif phase == 1:                           # (problem, 32-row block)
                 counts = [-(-int(r["B"]) // 32) for r in rows]
-            elif phase == 3:                           # (problem, position)
-                counts = [int(r["L"]) for r in rows]
-            else:                                      # (problem, n)
-                counts = [int(r["Nc"]) for r in rows]
+            else:                                      # (problem, 64 V-column block of the L F slice)
+                counts = [-(-int(r["L"]) * int(r["F"]) // (256 if r["flags"] & H.BIN_VEC4 else 64)) for r in rows]
             tiles = H.chunk_tiles(counts, 1)
             plan.launches.append(Launch("bin", phase, desc_tensor(rows, H.BIN_DTYPE), T(tiles), len(tiles)))
 
@@ -1565,10 +1564,14 @@ class HipPopulationEngine(PopulationEngine):
                                                         _nonarrow=1, _noadam=1))
                                     wg_dims.append((F, Lg, M))
                                     nbnsum_ext(o, bpid, 1, width)          # NbnDesc + part, one m slot
-                                    bw_bin.append(dict(bin_desc(o, bpid, n.id, col, width), Hm=hq, cs=csq,
-                                                       part=nbnsum_rows[o][bpid]["part"],
-                                                       dw=gptr(lay.w[n.id] + col), dbias=dbias if q == 0 else 0,
-                                                       adam=adam_ctx))
+                                    brow = dict(bin_desc(o, bpid, n.id, col, width), Hm=hq, cs=csq,
+                                                part=nbnsum_rows[o][bpid]["part"],
+                                                dw=gptr(lay.w[n.id] + col), dbias=dbias if q == 0 else 0,
+                                                adam=adam_ctx)
+                                    if (BIN_VEC4 and brow["F"] >= 4 and brow["ldw"] % 4 == 0 and brow["wc"] % 8 == 0
+                                            and brow["dw"] % 32 == 0 and (brow["L"] * brow["F"]) % 4 == 0):
+                                        brow["flags"] |= H.BIN_VEC4      # 4 columns per lane in bin_sw
+                                    bw_bin.append(brow)
                                     if adam_ctx:
                                         plan.adam_regions.append(((gptr(lay.w[n.id] + col) - self.g.data_ptr()) // 8,
                                                                   F, width, D))
@@ -1784,7 +1787,6 @@ class HipPopulationEngine(PopulationEngine):
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
             # (bin_s reads the bf16 weights before bin_wg's Adam step rewrites them)
             add_bin(3, bw_bin)
-            add_bin(4, bw_bin)
         # descriptor / tile tables are uploaded from pageable host memory: fence them before a launch can
         # read them.  Plans are built once per generation, so this costs nothing on the training hot path.
         tables.flush(plan.keep)

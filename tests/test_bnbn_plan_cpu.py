@@ -27,7 +27,7 @@ def _plan(name, binary, B=750):
 def test_binary_pairs_take_the_factorised_kernels():
     eng, pl = _plan("narrow_bn_ancestor", True)
     kinds = [(la.kind, la.arg) for la in pl.launches]
-    assert [a for k, a in kinds if k == "bin"] == [0, 1, 3, 4]
+    assert [a for k, a in kinds if k == "bin"] == [0, 1, 3]
     assert ("memset", None) not in kinds and any(k == "memset" for k, _ in kinds)
     # no DGRAD carries the BN-backward-sums epilogue any more, and no 7500-column slice GEMM remains
     for la in pl.launches:
