@@ -324,6 +324,58 @@ __global__ __launch_bounds__(1024) void nbn_fin_kernel(const NbnDesc* __restrict
     }
 }
 
+// Phase 7: the statistics of a K = 1 pair whose input is binary (a genotype batch of 0 / 1; the bnbn.hip
+// factorisation's training plans).  y takes v0 = act(b) where x = 0 and v1 = act(b + w) where x = 1, so with C1
+// ones among the R inputs the batch mean is (C0 v0 + C1 v1) / R and the biased variance (C0 (v0 - mu)^2 +
+// C1 (v1 - mu)^2) / R (two-pass form, fp64): one pass over the R inputs instead of the statistics-only narrow FWD
+// over the R x F outputs.  Moving statistics and mean / invstd as phase 2's first block.  tiles: (problem, ...).
+__global__ __launch_bounds__(256) void nbn_binstat_kernel(const NbnDesc* __restrict__ descs, const int4* __restrict__ tiles) {
+    __shared__ int red[4];
+    const NbnDesc& d = descs[tiles[blockIdx.x].x];
+    const int R = (int)d.R, F = (int)d.F, act = (int)d.act, flags = (int)d.flags, t = threadIdx.x;
+    const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(d.x);
+    // ones among the R inputs (K = 1: x is [R] contiguous; 16-B loads, four in flight)
+    int c = 0;
+    const int nv = (d.ldx == 1 && (d.x & 15) == 0) ? R / 8 : 0;
+    const uint4* __restrict__ Xv = reinterpret_cast<const uint4*>(X);
+    for (int i0 = t; i0 < nv; i0 += 4 * 256) {
+        uint4 u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = i0 + k * 256 < nv ? Xv[i0 + k * 256] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w4[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                c += (__uint_as_float(w4[h] << 16) > 0.5f) + (__uint_as_float(w4[h] & 0xffff0000u) > 0.5f);
+        }
+    }
+    for (int r = 8 * nv + t; r < R; r += 256) c += bf2f(X[(int64_t)r * d.ldx]) > 0.5f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((t & 63) == 0) red[t >> 6] = c;
+    __syncthreads();
+    const double C1 = (double)(red[0] + red[1] + red[2] + red[3]), C0 = (double)R - C1, Rd = (double)R;
+    const bf16_t* __restrict__ Wm = reinterpret_cast<const bf16_t*>(d.w);
+    const float* bias = reinterpret_cast<const float*>(d.bias);
+    const float eps = (float)d.eps, Rf = (float)R;
+    for (int f = t; f < F; f += 256) {
+        const float w = bf2f(Wm[f]), b = bias ? bias[f] : 0.f, zero = 0.f, one = 1.f;
+        const double v0 = nbn_y<1>(&zero, &w, b, act), v1 = nbn_y<1>(&one, &w, b, act);
+        const double mu = (C0 * v0 + C1 * v1) / Rd;
+        const float var = (float)((C0 * (v0 - mu) * (v0 - mu) + C1 * (v1 - mu) * (v1 - mu)) / Rd);
+        const float is = rsqrtf(var + eps);
+        const float mom = (float)d.momentum;
+        float* mm = reinterpret_cast<float*>(d.mm);
+        float* mv = reinterpret_cast<float*>(d.mv);
+        const float ub = (flags & 64) ? Rf / (Rf - 1.f) : Rf / (Rf - (1.f + eps));
+        mm[f] = mm[f] * mom + (float)mu * (1.f - mom);
+        mv[f] = mv[f] * mom + var * ub * (1.f - mom);
+        reinterpret_cast<float*>(d.mean)[f] = (float)mu;
+        reinterpret_cast<float*>(d.invstd)[f] = is;
+    }
+}
+
 void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {
     if (ntiles <= 0) return;
     const dim3 grid((unsigned)ntiles), block(256);
@@ -332,6 +384,10 @@ void launch_nbn(int phase, int k, uint64_t descs, uint64_t tiles, int64_t ntiles
     const int4* tp = as_ptr<const int4>(tiles);
     if (phase == 6) {
         hipLaunchKernelGGL(nbn_fin_kernel, grid, dim3(1024), 0, s, dp, tp);
+        return;
+    }
+    if (phase == 7) {
+        hipLaunchKernelGGL(nbn_binstat_kernel, grid, block, 0, s, dp, tp);
         return;
     }
 #define NBN_CASE(P_, K_) \

@@ -1244,6 +1244,11 @@ class HipPopulationEngine(PopulationEngine):
                                 bn_prefused.add((o, bnc))
                                 if n.id in nbn_src[o]:
                                     g_rows[-1]["flags"] |= H.GF_NOSTORE     # recomputed by nbn.hip
+                                    if bnc in binpair[o]:
+                                        # binary input: nbn phase 7 derives the statistics from the count
+                                        # of ones; nothing of this Dense runs in the FWD
+                                        g_rows.pop()
+                                        continue
                             elif n.id in nbn_src[o]:
                                 raise RuntimeError(f"organism {o}: Dense {n.id} fused with its BatchNormalization "
                                                    f"but not on the narrow statistics kernel")
@@ -1342,7 +1347,7 @@ class HipPopulationEngine(PopulationEngine):
                 add_gchain([r for r in gc_rows if r["_bn"]], H.GC_FSTAT)
             add_gchain(gc_rows, H.GC_FAPPLY)
             add_nbn([r for r in nbn_rows if not r.get("_bin")], 2)
-            add_nbn([r for r in nbn_rows if r.get("_bin")], 2, stats_only=True)
+            add_nbn([r for r in nbn_rows if r.get("_bin")], 7, stats_only=True)
             if bn_rows:
                 if train:
                     need0 = [i for i, need in enumerate(bn_stat) if need]      # (``sel`` is the organism filter)

@@ -35,10 +35,16 @@ def test_binary_pairs_take_the_factorised_kernels():
             d = np.frombuffer(la.descs.numpy().tobytes(), dtype=H.GEMM_DTYPE)
             assert not np.any(d["flags"] & H.GF_NBNSUM)
             assert not np.any(d["K"] == 7500) and not np.any(d["N"] == 7500)
-    # nbn phase 2: one statistics block per problem (the BN output is never written); phase 6 still runs
+    # nbn phase 7: one statistics block per problem from the count of ones (the BN output is never written,
+    # and the pair's Dense has no FWD launch at all: no statistics-only narrow kernel); phase 6 still runs
     nbn = [la for la in pl.launches if la.kind == "nbn"]
-    p2 = [la for la in nbn if la.arg[0] == 2]
-    assert len(p2) == 1 and p2[0].n == 2
+    assert not [la for la in nbn if la.arg[0] == 2]
+    p7 = [la for la in nbn if la.arg[0] == 7]
+    assert len(p7) == 1 and p7[0].n == 2
+    for la in pl.launches[:pl.fwd_count]:
+        if la.kind == "gemm3":
+            d = np.frombuffer(la.descs.numpy().tobytes(), dtype=H.GEMM_DTYPE)
+            assert not np.any(d["flags"] & H.GF_BNSTAT)
     assert any(la.arg[0] == 6 for la in nbn)
     # the factorised slice's dW is applied by bin_wg (Adam region), not by the arena pass
     assert any(r[2] == 7500 for r in pl.adam_regions)
