@@ -74,10 +74,13 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
 
 }  // namespace
 
-// tiles: (problem, n).  Four lanes per position (f = q, q + 4, ...), 64 positions per pass; the lanes' partial E
-// meet in a fixed-order pair exchange
+// tiles: (problem, n).  The row's weights reach LDS a pass of whole positions at a time (8-B loads, all in
+// flight, when the row is 8-B aligned); then four lanes per position (f = q, q + 4, ...) form E, their partials
+// meeting in a fixed-order pair exchange, and every lane adds its elements' Y0 terms to C0
+constexpr int BIN_STAGE = 8192;
 __global__ __launch_bounds__(256) void bin_prep_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
     __shared__ float sY0[256], sD[256], red[4];
+    __shared__ __attribute__((aligned(16))) bf16_t sw[BIN_STAGE];
     const int2 td = tiles[blockIdx.x];
     const BinDesc& d = descs[td.x];
     const int n = td.y, L = (int)d.L, F = (int)d.F, Nc = (int)d.Nc;
@@ -87,31 +90,38 @@ __global__ __launch_bounds__(256) void bin_prep_kernel(const BinDesc* __restrict
         sY0[t] = u.Y0;
         sD[t] = u.D;
     }
-    __syncthreads();
     const bf16_t* __restrict__ Wr = reinterpret_cast<const bf16_t*>(d.wc) + (int64_t)n * d.ldw;
+    const bool vec = (reinterpret_cast<uintptr_t>(Wr) & 7) == 0;
     float* __restrict__ E = reinterpret_cast<float*>(d.E);
+    const int ppass = (BIN_STAGE / F) & ~3;          // positions per pass (>= 32; a multiple of 4 keeps 8-B alignment)
     const int q = t & 3, pl = t >> 2;
     float c0 = 0.f;
-    for (int p0 = 0; p0 < L; p0 += 64) {
-        const int p = p0 + pl;
-        float e = 0.f;
-        if (p < L) {
-            const bf16_t* __restrict__ wp = Wr + p * F;
-            for (int f0 = q; f0 < F; f0 += 32) {         // eight loads in flight per lane
-                float wv[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) wv[k] = f0 + 4 * k < F ? bf2f(wp[f0 + 4 * k]) : 0.f;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int f = min(f0 + 4 * k, F - 1);
-                    e = fmaf(sD[f], wv[k], e);
-                    c0 = fmaf(sY0[f], wv[k], c0);
-                }
-            }
+    for (int p0 = 0; p0 < L; p0 += ppass) {
+        const int np = min(ppass, L - p0), j0 = p0 * F, nj = np * F;
+        __syncthreads();                              // (sY0 / sD written; the previous pass's readers done)
+        if (vec) {
+            const uint2* __restrict__ src = reinterpret_cast<const uint2*>(Wr + j0);
+            const int n4 = nj >> 2;
+#pragma unroll 8
+            for (int i = t; i < n4; i += 256) reinterpret_cast<uint2*>(sw)[i] = src[i];
+            for (int i = 4 * n4 + t; i < nj; i += 256) sw[i] = Wr[j0 + i];
+        } else {
+#pragma unroll 8
+            for (int i = t; i < nj; i += 256) sw[i] = Wr[j0 + i];
         }
-        e += __shfl_xor(e, 1, 64);
-        e += __shfl_xor(e, 2, 64);
-        if (q == 0 && p < L) E[(int64_t)p * Nc + n] = e;
+        __syncthreads();
+        for (int pp = pl; pp < np; pp += 64) {        // the four lanes of a position share pp (same wave)
+            const bf16_t* wp = sw + pp * F;
+            float e = 0.f;
+            for (int f = q; f < F; f += 4) {
+                const float wv = bf2f(wp[f]);
+                e = fmaf(sD[f], wv, e);
+                c0 = fmaf(sY0[f], wv, c0);
+            }
+            e += __shfl_xor(e, 1, 64);
+            e += __shfl_xor(e, 2, 64);
+            if (q == 0) E[(int64_t)(p0 + pp) * Nc + n] = e;
+        }
     }
     c0 = block_sum256(c0, red);
     if (t == 0) reinterpret_cast<float*>(d.C0)[n] = c0;
@@ -156,12 +166,15 @@ __global__ __launch_bounds__(256) void bin_fwd_kernel(const BinDesc* __restrict_
     }
 }
 
-// tiles: (problem, 64 V-column block of the slice): lane -> columns j = pF + f .. + V - 1, wave -> rows n = wave,
-// wave + 4, ...  V = 4 (BIN_VEC4: 16-B fp32 / 8-B 16-bit accesses) when the slice's columns, row stride and arena
+// tiles: (problem, (64 V-column block) * ns + split): lane -> columns j = pF + f .. + V - 1, wave -> rows
+// n = r0 + wave, r0 + wave + 4, ... of the split's row range [r0, r1)  V = 4 (BIN_VEC4: 16-B fp32 / 8-B 16-bit accesses) when the slice's columns, row stride and arena
 // offset are multiples of 4 and F >= 4 (a lane's columns span at most two positions), else V = 1.
 // MM: Adam moment storage (common.h).  Explicit fmaf: the store and the fused-Adam branches must round alike (the
 // arena pass and the in-place update see the same gradient)
-constexpr int BIN_NL = 4, BIN_UNROLL = 2, BIN_VEC4 = 4;
+#ifndef SERANN_BIN_UNROLL
+#define SERANN_BIN_UNROLL 2
+#endif
+constexpr int BIN_NL = 4, BIN_UNROLL = SERANN_BIN_UNROLL, BIN_VEC4 = 4;
 __device__ __forceinline__ float bin_grad(float Y0, float Dd, float c, float h) { return fmaf(Dd, h, Y0 * c); }
 
 template <int V> __device__ __forceinline__ void ldv_bf(const bf16_t* p, float* x) {
@@ -187,9 +200,9 @@ template <int MM, int V> __device__ __forceinline__ void ldv_m(const void* b, in
 }
 
 template <int MM, int V>
-__device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nl, const int* pc, const float* Y0,
+__device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nb, int Nc, const int* pc, const float* Y0,
                                             const float* Dd, float* s1, float* st) {
-    const int Nc = (int)d.Nc, L = (int)d.L;
+    const int L = (int)d.L;
     const int64_t ldw = d.ldw;
     const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(d.wc) + j;
     const long long* __restrict__ Hq = reinterpret_cast<const long long*>(d.Hm);       // Q40 [Nc][L]
@@ -198,7 +211,7 @@ __device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nl, con
     // a lane's columns lie in positions pc[0] and pc[0] + 1 (F >= V)
     const int pa = pc[0], pb = min(pc[0] + 1, L - 1);
     if (!d.adam) {
-        for (int n = nl; n < Nc; n += BIN_NL) {
+        for (int n = nb; n < Nc; n += BIN_NL) {
             const float ha = fx_f(Hq[(int64_t)n * L + pa]), hb = fx_f(Hq[(int64_t)n * L + pb]), c = fx_f(csq[n]);
             float w[V];
             ldv_bf<V>(W + n * ldw, w);
@@ -223,7 +236,7 @@ __device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nl, con
     const float b1 = ac.b1, b2 = ac.b2, eps = ac.eps;
     void* __restrict__ Mo = reinterpret_cast<void*>(ac.m);
     void* __restrict__ Vo = reinterpret_cast<void*>(ac.v);
-    for (int n0 = nl; n0 < Nc; n0 += BIN_NL * BIN_UNROLL) {
+    for (int n0 = nb; n0 < Nc; n0 += BIN_NL * BIN_UNROLL) {
         float w[BIN_UNROLL][V], p_[BIN_UNROLL][V], m_[BIN_UNROLL][V], v_[BIN_UNROLL][V];
         float ha[BIN_UNROLL], hb[BIN_UNROLL], c[BIN_UNROLL];
 #pragma unroll
@@ -268,19 +281,21 @@ __device__ __forceinline__ void bin_sw_cols(const BinDesc& d, int j, int nl, con
 }
 
 template <int V>
-__device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb) {
+__device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb, int sp) {
     constexpr int COLS = 64 * V;
     __shared__ float red[256], sN1[256], sS1[BIN_NL][COLS], sSt[BIN_NL][COLS];
     const int F = (int)d.F, Nc = (int)d.Nc, L = (int)d.L, M = (int)d.B, W = L * F;
-    const int t = threadIdx.x, lane = t & 63, nl = t >> 6;
+    const int t = threadIdx.x, lane = t & 63;
+    const int nl = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform: row indices and cs in scalar registers
     const int j0 = jb * COLS, j = j0 + lane * V;
-    if (jb == 0 && d.dbias) {                         // the consumer's bias gradient: cs, once per problem
+    const int ns = (int)d.ns, r0 = (int)((int64_t)sp * Nc / ns), r1 = (int)((int64_t)(sp + 1) * Nc / ns);
+    if (jb == 0 && sp == 0 && d.dbias) {             // the consumer's bias gradient: cs, once per problem
         const long long* __restrict__ csq = reinterpret_cast<const long long*>(d.cs);
         for (int n = t; n < Nc; n += 256) fx_add(reinterpret_cast<long long*>(d.dbias) + n, fx_f(csq[n]));
     }
     // N1 of the block's positions [pl, pl + np): thread (mi, pi) sums rows mi, mi + nm, ... of position pl + pi
     const int pl = j0 / F, np = min(L - 1, (j0 + COLS - 1) / F) - pl + 1, nm = 256 / np;
-    {
+    if (sp == 0) {                                    // (block-uniform)
         const bf16_t* __restrict__ g = reinterpret_cast<const bf16_t*>(d.g) + pl;
         const int pi = t % np, mi = t / np;
         float c = 0.f;
@@ -296,21 +311,20 @@ __device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb) {
     }
     int pc[V];
     float Y0[V], Dd[V], s1[V], st[V];
-    BinUnit u[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) {
         const int jc = min(j + k, W - 1);
         pc[k] = jc / F;
-        u[k] = bin_unit(d, jc - pc[k] * F);
-        Y0[k] = u[k].Y0;
-        Dd[k] = u[k].D;
+        const BinUnit u = bin_unit(d, jc - pc[k] * F);     // (recomputed for the sums: fewer live registers)
+        Y0[k] = u.Y0;
+        Dd[k] = u.D;
         s1[k] = st[k] = 0.f;
     }
     if (j < W) {
         if (d.adam && reinterpret_cast<const AdamCtx*>(d.adam)->mode == MOM_16)
-            bin_sw_cols<MOM_16, V>(d, j, nl, pc, Y0, Dd, s1, st);
+            bin_sw_cols<MOM_16, V>(d, j, r0 + nl, r1, pc, Y0, Dd, s1, st);
         else
-            bin_sw_cols<MOM_F32, V>(d, j, nl, pc, Y0, Dd, s1, st);
+            bin_sw_cols<MOM_F32, V>(d, j, r0 + nl, r1, pc, Y0, Dd, s1, st);
     }
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -325,11 +339,13 @@ __device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb) {
         if (j + k >= W) break;
         const float S1 = ((sS1[0][c] + sS1[1][c]) + sS1[2][c]) + sS1[3][c];
         const float St = ((sSt[0][c] + sSt[1][c]) + sSt[2][c]) + sSt[3][c];
-        const float N1 = sN1[pc[k] - pl], N0 = (float)M - N1, s0 = St - S1;
-        const BinUnit& q = u[k];
+        // (the count terms once: in split 0's slot; the S terms are linear, so the slots add up in phase 6)
+        const float N1 = sp == 0 ? sN1[pc[k] - pl] : 0.f, N0 = sp == 0 ? (float)M - sN1[pc[k] - pl] : 0.f;
+        const float s0 = St - S1;
+        const BinUnit q = bin_unit(d, j + k - pc[k] * F);
         // the eight sums of gemm3.hip's GF_NBNSUM epilogue over the column's B rows (x = g in {0, 1}):
         //   [0] dy  [1] dy xhat  [2] a dy  [3] a xhat  [4] a  [5] a x dy  [6] a x xhat  [7] a x
-        float* __restrict__ o = reinterpret_cast<float*>(d.part) + (int64_t)(j + k) * NBN_NSUM;
+        float* __restrict__ o = reinterpret_cast<float*>(d.part) + ((int64_t)sp * W + j + k) * NBN_NSUM;
         *reinterpret_cast<float4*>(o) = make_float4(St, q.xh0 * s0 + q.xh1 * S1, q.a0 * s0 + q.a1 * S1,
                                                     q.a0 * q.xh0 * N0 + q.a1 * q.xh1 * N1);
         *reinterpret_cast<float4*>(o + 4) = make_float4(q.a0 * N0 + q.a1 * N1, q.a1 * S1, q.a1 * q.xh1 * N1, q.a1 * N1);
@@ -339,10 +355,11 @@ __device__ __forceinline__ void bin_sw_block(const BinDesc& d, int jb) {
 __global__ __launch_bounds__(256) void bin_sw_kernel(const BinDesc* __restrict__ descs, const int2* __restrict__ tiles) {
     const int2 td = tiles[blockIdx.x];
     const BinDesc& d = descs[td.x];
+    const int ns = (int)d.ns, jb = td.y / ns;
     if (d.flags & BIN_VEC4)
-        bin_sw_block<4>(d, td.y);
+        bin_sw_block<4>(d, jb, td.y - jb * ns);
     else
-        bin_sw_block<1>(d, td.y);
+        bin_sw_block<1>(d, jb, td.y - jb * ns);
 }
 
 void launch_bin(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream) {

@@ -193,7 +193,8 @@ struct BinDesc {
     int64_t g, w, bias, gamma, beta, mean, invstd, act, flags;
     int64_t wc, ldw, Nc, L, F, B;
     int64_t E, C0, slab, Hm, cs, part, dw, dbias, adam;
+    int64_t ns;   // bin_sw row splits: split s sums rows [s Nc / ns, (s + 1) Nc / ns) into part slot s
 };
-// phase 0 bin_prep (problem, n), 1 bin_fwd (problem, 32 rows), 3 bin_sw (problem, 64 slice columns)
+// phase 0 bin_prep (problem, n), 1 bin_fwd (problem, 32 rows), 3 bin_sw (problem, column block * ns + split)
 void launch_bin(int phase, uint64_t descs, uint64_t tiles, int64_t ntiles, uint64_t stream);
 

@@ -126,6 +126,7 @@ FUSE_NBN = os.environ.get("SERANN_FUSE_NBN", "1") != "0"
 # binary-genotype factorisation of raw-genotype Dense -> BN pairs read by a merged-Dense K slice (csrc/hip/bnbn.hip)
 BINARY_NBN = os.environ.get("SERANN_BINARY_NBN", "1") != "0"
 BIN_VEC4 = os.environ.get("SERANN_BIN_VEC4", "1") != "0"
+BIN_SW_BLOCKS = int(os.environ.get("SERANN_BIN_SW_BLOCKS", "1024"))   # row-split target of a bin_sw launch
 # fused pairs whose BN output feeds one LDS-tiled DGRAD: BN backward sums in that DGRAD's epilogue (nbn phase 6)
 NBN_SUM = os.environ.get("SERANN_NBNSUM", "1") != "0"
 
@@ -1057,10 +1058,25 @@ class HipPopulationEngine(PopulationEngine):
                 counts = [int(r["Nc"]) for r in rows]
             elif phase == 1:                           # (problem, 32-row block)
                 counts = [-(-int(r["B"]) // 32) for r in rows]
-            else:                                      # (problem, 64 V-column block of the L F slice)
-                counts = [-(-int(r["L"]) * int(r["F"]) // (256 if r["flags"] & H.BIN_VEC4 else 64)) for r in rows]
+            else:                                      # (problem, (64 V-column block) * ns + split)
+                counts = [-(-int(r["L"]) * int(r["F"]) // (256 if r["flags"] & H.BIN_VEC4 else 64)) * int(r["ns"])
+                          for r in rows]
             tiles = H.chunk_tiles(counts, 1)
             plan.launches.append(Launch("bin", phase, desc_tensor(rows, H.BIN_DTYPE), T(tiles), len(tiles)))
+
+        def add_bin_sw(rows):
+            """bin_sw over this depth's factorised slices.  A launch of few column blocks (a lone organism's
+            slice) splits its rows too, towards BIN_SW_BLOCKS blocks of >= 32 rows each; split s writes its
+            partial sums into NbnDesc::part slot s, which phase 6 adds with the others."""
+            if not rows:
+                return
+            jbl = [-(-int(r["L"]) * int(r["F"]) // (256 if r["flags"] & H.BIN_VEC4 else 64)) for r in rows]
+            want = -(-BIN_SW_BLOCKS // sum(jbl))
+            for r in rows:
+                r["ns"] = max(1, min(want, int(r["Nc"]) // 32))
+                nbnsum_ext(r["_o"], r["_bid"], 128 * r["ns"], int(r["L"]) * int(r["F"]))   # ns m slots
+                r["part"] = nbnsum_rows[r["_o"]][r["_bid"]]["part"]
+            add_bin(3, rows)
 
         def nbnsum_ext(o, bid, M_, N_):
             """Device NbnDesc (with its partial-sum workspace) for the GF_NBNSUM DGRAD of pair ``bid``."""
@@ -1568,11 +1584,9 @@ class HipPopulationEngine(PopulationEngine):
                                                         N=Lg, K=M, flags=(H.GF_VEC_A if F % 8 == 0 else 0),
                                                         _nonarrow=1, _noadam=1))
                                     wg_dims.append((F, Lg, M))
-                                    nbnsum_ext(o, bpid, 1, width)          # NbnDesc + part, one m slot
                                     brow = dict(bin_desc(o, bpid, n.id, col, width), Hm=hq, cs=csq,
-                                                part=nbnsum_rows[o][bpid]["part"],
                                                 dw=gptr(lay.w[n.id] + col), dbias=dbias if q == 0 else 0,
-                                                adam=adam_ctx)
+                                                adam=adam_ctx, _o=o, _bid=bpid)   # (part, ns: add_bin_sw)
                                     if (BIN_VEC4 and brow["F"] >= 4 and brow["ldw"] % 4 == 0 and brow["wc"] % 8 == 0
                                             and brow["dw"] % 32 == 0 and (brow["L"] * brow["F"]) % 4 == 0):
                                         brow["flags"] |= H.BIN_VEC4      # 4 columns per lane in bin_sw
@@ -1790,8 +1804,7 @@ class HipPopulationEngine(PopulationEngine):
                         r[k_] = r[k_].resolve(base_)
                 plan.launches.append(Launch("memset", (base_, 2 * wsz.numel()), None, None, 0))
             add_gemm(H.MODE_WGRAD, wg_rows, wg_dims)
-            # (bin_s reads the bf16 weights before bin_wg's Adam step rewrites them)
-            add_bin(3, bw_bin)
+            add_bin_sw(bw_bin)
         # descriptor / tile tables are uploaded from pageable host memory: fence them before a launch can
         # read them.  Plans are built once per generation, so this costs nothing on the training hot path.
         tables.flush(plan.keep)

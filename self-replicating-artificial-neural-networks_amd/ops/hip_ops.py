@@ -39,7 +39,7 @@ SPLITFIN_ELEMS = 2048  # aux.hip: outputs per block of the split-K finalize kern
 WGFIN_DTYPE = np.dtype([(f, _I) for f in ["ws", "out", "adam", "M", "N", "C", "Cp", "S", "ldo", "flags"]])
 BIN_DTYPE = np.dtype([(f, _I) for f in ["g", "w", "bias", "gamma", "beta", "mean", "invstd", "act", "flags", "wc", "ldw",
                                         "Nc", "L", "F", "B", "E", "C0", "slab", "Hm", "cs", "part", "dw", "dbias",
-                                        "adam"]])
+                                        "adam", "ns"]])
 BIN_VEC4 = 4           # bnbn.hip BinDesc::flags: bin_sw reads / writes 4 columns per lane
 WGFIN_ELEMS = 64       # aux.hip: outputs per block of the split WGRAD finalize kernel
 CONVPOOL_DTYPE = np.dtype([(f, _I) for f in ["x", "w", "bias", "y", "idx", "dy", "dw", "dbias", "B", "H", "W", "F",

@@ -48,9 +48,14 @@ def test_binary_pairs_take_the_factorised_kernels():
     assert any(la.arg[0] == 6 for la in nbn)
     # the factorised slice's dW is applied by bin_wg (Adam region), not by the arena pass
     assert any(r[2] == 7500 for r in pl.adam_regions)
-    # part buffers of phase 6 hold one m slot
+    # part buffers of phase 6 hold one m slot per bin_sw row split (two organisms: few column blocks, so the
+    # 152 rows are split towards BIN_SW_BLOCKS blocks of >= 32 rows)
     rows = np.frombuffer([la for la in nbn if la.arg[0] == 6][0].descs.numpy().tobytes(), dtype=H.NBN_DTYPE)
-    assert np.all(rows["mtiles"] == 1) and np.all(rows["np"] == 100)
+    sw = [la for la in pl.launches if la.kind == "bin" and la.arg == 3][0]
+    brows = np.frombuffer(sw.descs.numpy().tobytes(), dtype=H.BIN_DTYPE)
+    cols = np.where(brows["flags"] & H.BIN_VEC4, 256, 64)
+    assert np.all(brows["ns"] == 4) and sw.n == int(np.sum(4 * -(-brows["L"] * brows["F"] // cols)))
+    assert np.all(rows["mtiles"] == 4) and np.all(rows["np"] == 100)
 
 
 def test_non_binary_genotypes_keep_the_nbnsum_path():
