@@ -2945,6 +2945,78 @@ bool gemm3_launch_part2(int mode, int variant, dim3 grid, dim3 block, hipStream_
 #endif
 
 #if G3_PART(3)
+// ==================================================================================================
+// Shared-input FWD ("one input, many filter banks").  Every organism's first layer reads the same raw input batch
+// (experiment_worker.py:226-227: one X / g batch for the whole population), so the planner materialises one im2col
+// matrix per (input, kernel geometry) (hip_engine.py raw_conv_imcol) and its first-layer convolutions are [M x K8]
+// x [K8 x F] problems over the SAME A.  Filter banks are small (layer_transitions.py:39: F = 2^clip(N(4.5, 1)),
+// mostly 8 - 32), so one problem per block would re-read A for every organism and fill half-empty MFMA tiles with
+// a few k steps of work per block.  Here a block holds its 256 rows of A in registers (KS k steps of 32; the
+// matrix's row stride C = K8 <= 32 KS) and walks a run of problems that share it -- tile (first problem, m tile,
+// problem count): per problem only its [N x K] filter bank (L2-resident) is loaded, multiplied, BN statistics
+// accumulated (GF_BNUSTAT) and the tile stored through the per-wave LDS stage (16-B row-contiguous stores).
+// Every problem of a run has N <= 16 NT (one column tile) and plain bf16 output (no GF_ACCUM / GF_OUT_F32).
+template <int NT, int KS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void g3_shared_fwd_kernel(const GemmDesc* __restrict__ descs, const int4* __restrict__ tiles) {
+    constexpr int RT = 4, WROWS = RT * 16, BNB = NT * 16;
+    __shared__ __attribute__((aligned(16))) bf16_t ostage[4 * WROWS * BNB];
+    __shared__ float bnred[4 * 2 * BNB];
+    const int4 td = tiles[blockIdx.x];
+    const int nprob = td.z;
+    const GemmDesc& d0 = descs[td.x];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kg = (lane >> 4) * 8;
+    const int M = (int)d0.M, C = (int)d0.C;
+    const int m_w = td.y * 4 * WROWS + wave * WROWS;
+    const rsrc_t rA = mkrsrc(d0.a, (int64_t)M * C * 2);
+    Frag fa[KS][RT];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const int row = m_w + i * 16 + r16, k = s * 32 + kg;
+            fa[s][i].u = bl16(rA, (row < M && k < C) ? row * C + k : -1);
+        }
+    const int nrows = min(WROWS, M - m_w);
+    for (int q = 0; q < nprob; ++q) {
+        const GemmDesc& d = descs[td.x + q];
+        const int N = (int)d.N, K = (int)d.K, act = (int)d.act, flags = (int)d.flags;
+        const rsrc_t rB = mkrsrc(d.b, (int64_t)N * K * 2);
+        const int brow = min(r16, N - 1) * K;
+        f32x4_t acc[RT][NT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = s * 32 + kg;
+            Frag fb[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = j * 16 + r16;
+                fb[j].u = bl16(rB, (k < K && n < N) ? brow + j * 16 * K + k : -1);
+                if (k + 8 > K) fb[j].u = splice(fb[j].u, make_uint4(0, 0, 0, 0), K - k);
+            }
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i].v, fb[j].v, acc[i][j], 0, 0, 0);
+        }
+        const float* bias = reinterpret_cast<const float*>(d.bias);
+        if (flags & GF_BNUSTAT) {
+            bn_ustat_flush<RT, NT, 1>(d, acc, [&](int i, int rr) { return m_w + i * 16 + rr < M; }, 0, N, bias, act,
+                                      bnred, wave, lane, N);
+            __syncthreads();                             // (bnred is re-used by the next problem)
+        }
+        if (nrows > 0)
+            wave_store_rows<RT, NT>(&ostage[wave * WROWS * BNB], reinterpret_cast<bf16_t*>(d.out), m_w, nrows, N, false,
+                                    acc, bias, act, lane);
+    }
+}
+
 // part 3: narrow FWD, single-step and direct-fragment FWD / DGRAD
 bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
                           const int4* tp) {
@@ -2959,6 +3031,18 @@ bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_
         else throw std::runtime_error("gemm3: unknown narrow FWD variant " + std::to_string(variant));
         SERANN_CHECK(hipGetLastError());
         return true;
+    }
+    if (mode == MODE_FWD && variant > 5100 && variant < 5200) {
+        const int v = variant - 5100;
+#define SH3(NT_, KS_)                                                                                   \
+    if (v == NT_ + 10 * KS_) {                                                                          \
+        hipLaunchKernelGGL((g3_shared_fwd_kernel<NT_, KS_>), grid, block, 0, s, dp, tp);                \
+        SERANN_CHECK(hipGetLastError());                                                                \
+        return true;                                                                                    \
+    }
+        SH3(1, 1) SH3(2, 1) SH3(4, 1) SH3(1, 2) SH3(2, 2) SH3(4, 2) SH3(1, 3) SH3(2, 3) SH3(4, 3)
+#undef SH3
+        throw std::runtime_error("gemm3: unknown shared-input FWD variant " + std::to_string(variant));
     }
     if (variant >= 5000) {
         const int v = variant - 5000;

@@ -1244,7 +1244,7 @@ class HipPopulationEngine(PopulationEngine):
                         elif ic is not None:
                             g_rows.append(dict(a=ic["buf"].data_ptr(), b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=OH,
                                                W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1, SH=1, SW=1, M=M, N=F,
-                                               K=K, act=act, flags=flags))
+                                               K=K, act=act, flags=flags, _imcol=1))
                             bnustat(o, n, g_rows[-1], M, F, K)
                         else:
                             g_rows.append(dict(a=xin, b=wptr_bf(lay.w[n.id]), out=out, bias=bias, H=Hh, W=Ww, C=C, OH=OH,

@@ -572,6 +572,8 @@ def gemm3_block(mode: int, variant: int):
     if mode == MODE_WGRAD:
         v = variant % 1000000
         return (v // 1000, (v % 1000) % 500)
+    if mode == MODE_FWD and 5100 < variant < 5200:
+        return (256, 16 * (variant % 10))           # shared-input FWD: 256 rows, one column tile
     if 7000 < variant % 10000 < 7300 and variant < 20000:
         return (128, variant % 10000 - 7000)
     if 8000 < variant % 10000 < 8300 and variant < 20000:
@@ -706,6 +708,60 @@ def narrow_k(geo: dict, mode: int, M: int, N: int, K: int):
     return None
 
 
+# Shared-input FWD (gemm3.hip g3_shared_fwd_kernel): first-layer problems over one materialised im2col matrix
+# (rows annotated ``_imcol`` by the engine) run as runs of problems per 256-row block; a launch aims at this many
+# blocks (problem runs are split until it is reached, or one problem per run)
+SHARED_FWD_BLOCKS = int(_os.environ.get("SERANN_SHARED_FWD_BLOCKS", "1024"))
+SHARED_FWD_MAXC, SHARED_FWD_MAXN = 96, 64
+# problems per matrix to share (1: every eligible row, so the kernel that computes a problem -- and its bits -- do
+# not depend on which organisms share its launch, shard or stream group)
+SHARED_FWD_MIN = int(_os.environ.get("SERANN_SHARED_FWD_MIN", "1"))
+
+
+def shared_fwd_ok(r: dict, M: int, N: int, K: int) -> bool:
+    """True when FWD row ``r`` may join a shared-input run: an im2col first layer (``_imcol``) whose row stride
+    (C = K8) fits the kernel's 3 register-held k steps, one column tile of at most 64 filters, plain bf16 output."""
+    if "shared" in _OFF or not r.get("_imcol"):
+        return False
+    flags = int(r.get("flags", 0))
+    return (int(r["C"]) <= SHARED_FWD_MAXC and N <= SHARED_FWD_MAXN and K <= int(r["C"])
+            and not flags & (GF_ACCUM | GF_OUT_F32 | GF_SPLITWS) and not r.get("_force_tiled") and not r.get("_split"))
+
+
+def shared_fwd_variant(C: int, maxN: int) -> int:
+    """gemm3.hip g3_shared_fwd_kernel<NT, KS> encoding: 5100 + 10 * KS + NT."""
+    nt = 1 if maxN <= 16 else (2 if maxN <= 32 else 4)
+    return 5100 + 10 * -(-int(C) // 32) + nt
+
+
+def shared_fwd_tiles(items) -> tuple:
+    """Tile table of one shared-input FWD launch: ``items`` (row, (M, N, K)) reordered so the problems of one
+    im2col matrix are consecutive, then per matrix its m tiles x runs of problems, the runs of one m tile on one
+    XCD (they read the same A rows).  Returns (items, int32 (n, 4) tiles (first problem, m tile, count, 0))."""
+    order = sorted(range(len(items)), key=lambda i: (int(items[i][0]["a"]), i))
+    items = [items[i] for i in order]
+    tl = []
+    p = 0
+    while p < len(items):
+        a = int(items[p][0]["a"])
+        q = p
+        while q < len(items) and int(items[q][0]["a"]) == a:
+            q += 1
+        n, M = q - p, int(items[p][1][0])
+        mt = -(-M // 256)
+        nch = max(1, min(n, -(-SHARED_FWD_BLOCKS // mt)))
+        per = -(-n // nch)
+        starts = np.arange(p, q, per)
+        t_ = np.empty((mt, len(starts), 4), np.int64)
+        t_[..., 0] = starts[None, :]
+        t_[..., 1] = np.arange(mt)[:, None]
+        t_[..., 2] = np.minimum(per, q - starts)[None, :]
+        t_[..., 3] = 0
+        tl.append(xcd_swizzle(t_.reshape(-1, 4), len(starts)))
+        p = q
+    return items, np.concatenate(tl).astype(np.int32)
+
+
 TILED_BNS = (64, 128, 160, 192)               # gemm3.hip g3_tiled_kernel instantiations
 
 
@@ -749,12 +805,22 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
     marked ``_split`` = number of splits, plus GF_SPLITWS and kper); the caller provides the fp32
     workspace (``aux``) and runs splitk_finalize after the launch."""
     groups = {}
+    # shared-input runs: im2col first layers of >= 2 problems over one matrix (widest filter bank sets the variant)
+    share = {}
+    if mode == MODE_FWD:
+        for r, (M, N, K) in zip(rows, dims):
+            if narrow_k(r, mode, M, N, K) is None and shared_fwd_ok(r, M, N, K):
+                n_, mx = share.get(int(r["a"]), (0, 0))
+                share[int(r["a"])] = (n_ + 1, max(mx, N))
     for r, dm in zip(rows, dims):
         M, N, K = dm
         v = None
         nk = narrow_k(r, mode, M, N, K) if mode in (MODE_FWD, MODE_WGRAD) and not r.get("_nonarrow") else None
+        sh = share.get(int(r.get("a", 0))) if share and nk is None and shared_fwd_ok(r, M, N, K) else None
         if r.get("_force_tiled"):
             v = 7000 + tiled_bn(N)                # K slice of a concat input: LDS-tiled + workspace
+        elif sh is not None and sh[0] >= SHARED_FWD_MIN:
+            v = shared_fwd_variant(int(r["C"]), sh[1])
         elif nk is not None:
             # + 100: LDS-staged rows when the narrow kernel's row width (N, or F for WGRAD) is not a
             # multiple of 8 (unaligned 16-B row chunks); measured faster for K <= 2 (Dense on the raw
@@ -821,6 +887,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 nb = -(-nrows // per)
                 tl.append(np.stack([np.full(nb, p), np.arange(nb), np.zeros(nb, int), np.zeros(nb, int)], 1))
             tiles = np.concatenate(tl).astype(np.int32)
+        elif mode == MODE_FWD and 5100 < v < 5200:
+            items, tiles = shared_fwd_tiles(items)
         elif 2000 <= v < 3000 and mode in (MODE_FWD, MODE_DGRAD):
             nt, rt = v % 10, (v // 10) % 10
             tm, bn = 64 * rt, 16 * nt

@@ -655,3 +655,64 @@ def test_fwd_epilogue_bn_statistics(shape):
     sums = (w4[..., 0].double() + w4[..., 1].double() / 2.0 ** 32).sum(0)
     torch.testing.assert_close(sums[:Fo], yv.sum(0).cpu(), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(sums[Fo:], (yv * yv).sum(0).cpu(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("geom", [(28, 28, 5, 5, 1), (28, 28, 3, 3, 2), (28, 28, 7, 7, 1), (24, 20, 9, 9, 1),
+                                  (100, 1, 5, 1, 1)])
+def test_shared_input_fwd_many_filter_banks(geom, monkeypatch):
+    """g3_shared_fwd_kernel: first layers of several organisms over ONE im2col matrix of the shared input batch
+    (filter banks of 8 - 60 filters, mixed activations, BN statistics in the epilogue for some): each output
+    against the fp32 convolution, the statistics against the stored outputs, and bitwise against the same
+    problems run one by one on the unshared kernels (direct single-step / LDS-tiled)."""
+    Hh, Ww, KH, KW, S = geom
+    B = 40
+    OH, OW = (Hh - KH) // S + 1, (Ww - KW) // S + 1
+    M, K = B * OH * OW, KH * KW
+    K8 = -(-K // 8) * 8
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(B, 1, Hh, Ww, device=DEV, generator=g).bfloat16()
+    cols = F.unfold(x.float().cpu(), (KH, KW), stride=S)                 # [B, K, OH*OW], taps (kh, kw)
+    A = torch.zeros(M, K8)
+    A[:, :K] = cols.permute(0, 2, 1).reshape(M, K)
+    A = H.padded(A.to(DEV).bfloat16())
+    banks = [(16, "relu", True), (8, "linear", False), (32, "sigmoid", True), (13, "relu", False), (60, "linear", True)]
+    ws_, bs_, rows = [], [], []
+    for Fo, act, stat in banks:
+        w = H.padded((torch.randn(Fo, K, device=DEV, generator=g) / math.sqrt(K)).bfloat16())
+        b = H.padded(torch.randn(Fo, device=DEV, generator=g) * 0.3)
+        ws_.append(w)
+        bs_.append(b)
+        rows.append(dict(a=A.data_ptr(), b=w.data_ptr(), bias=b.data_ptr(), M=M, N=Fo, K=K, C=K8, H=OH, W=OW, OH=OH,
+                         OW=OW, F=Fo, KH=1, KW=1, SH=1, SW=1, act=H.ACT_CODES[act], flags=H.GF_BNUSTAT if stat else 0,
+                         _imcol=1))
+    results = []
+    for off in (set(), {"shared"}):
+        monkeypatch.setattr(H, "_OFF", off)
+        plans = H.gemm3_plan(H.MODE_FWD, [dict(r) for r in rows], [(M, r["N"], K) for r in rows])
+        assert any(5100 < v < 5200 for v, _, _ in plans) == (not off)
+        outs = []
+        for r in rows:
+            y = H.padded(torch.zeros(M, r["N"], dtype=torch.bfloat16, device=DEV))
+            wsb = H.operand(H.bn_ws_words(r["N"]), torch.int64, DEV)
+            wsb.zero_()
+            outs.append((y, wsb))
+        run = [dict(r, out=y.data_ptr(), aux=wsb.data_ptr() if r["flags"] else 0) for r, (y, wsb) in zip(rows, outs)]
+        if off:
+            for r in run:                                  # one by one on the usual kernels (outputs only)
+                _run_gemm(H.MODE_FWD, [dict(r, flags=0, aux=0)], [(M, r["N"], K)])
+        else:
+            _run_gemm(H.MODE_FWD, run, [(M, r["N"], K) for r in run])
+        results.append(outs)
+    for i, ((Fo, act, stat), w, b) in enumerate(zip(banks, ws_, bs_)):
+        y, wsb = results[0][i]
+        ref = ref_conv2d(x, w.view(Fo, 1, KH, KW), b, S)                    # [B, F, OH, OW]
+        ref = {"relu": torch.relu, "sigmoid": torch.sigmoid, "linear": lambda t: t}[act](ref)
+        got = y.view(B, OH, OW, Fo).permute(0, 3, 1, 2).float()
+        assert _rel(got, ref) < 6e-3, (i, _rel(got, ref))
+        assert torch.equal(y, results[1][i][0]), f"bank {i}: shared and unshared outputs differ"
+        if stat:
+            yv = y.double()
+            w4 = wsb[:H.bn_ws_words(Fo)].reshape(H.BN_WS_STRIPES, 2 * Fo, 2).cpu()
+            sums = (w4[..., 0].double() + w4[..., 1].double() / 2.0 ** 32).sum(0)
+            torch.testing.assert_close(sums[:Fo], yv.sum(0).cpu(), rtol=1e-5, atol=1e-3)
+            torch.testing.assert_close(sums[Fo:], (yv * yv).sum(0).cpu(), rtol=1e-5, atol=1e-3)

@@ -283,3 +283,51 @@ def test_wgrad_row_groups_are_per_problem():
     for r, d in zip(rows, probs):
         (v, rws, tiles), = H.gemm3_plan(H.MODE_WGRAD, [dict(r)], [d])
         assert (v, rws[0]["flags"], sorted(set(int(x) for x in tiles[:, 3]))) == full[r["out"]]
+
+
+def _imcol_rows(specs):
+    """FWD rows of first-layer convolutions over materialised im2col matrices: (matrix id, M, K8, K, N)."""
+    rows, dims = [], []
+    for i, (a, M, C, K, N) in enumerate(specs):
+        rows.append(dict(a=1000 * (a + 1), out=10 ** 6 * (i + 1), M=M, N=N, K=K, C=C, H=1, W=M, OH=1, OW=M,
+                         KH=1, KW=1, SH=1, SW=1, flags=0, _imcol=1))
+        dims.append((M, N, K))
+    return rows, dims
+
+
+def test_shared_input_fwd_runs_cover_every_tile_once():
+    """Shared-input FWD (g3_shared_fwd_kernel): the problems of one im2col matrix are consecutive in the launch's
+    descriptor table and every (problem, 256-row tile) is computed by exactly one run."""
+    specs = [(0, 432000, 32, 25, 16), (1, 126750, 16, 9, 16), (0, 432000, 32, 25, 8), (2, 300000, 56, 49, 32),
+             (0, 432000, 32, 25, 16), (1, 126750, 16, 9, 16), (2, 300000, 56, 49, 8), (3, 9000, 88, 81, 60)]
+    rows, dims = _imcol_rows(specs)
+    rows.append(dict(rows[0], _imcol=0, out=5))          # not an im2col first layer: the usual kernels
+    dims.append(dims[0])
+    plans = H.gemm3_plan(H.MODE_FWD, [dict(r) for r in rows], dims)
+    shared = [(v, rws, t) for v, rws, t in plans if 5100 < v < 5200]
+    assert sorted(v for v, _, _ in shared) == [5111, 5122, 5134]     # (NT, KS) by the widest bank, K8
+    seen = {}
+    for v, rws, tiles in shared:
+        a = [r["a"] for r in rws]
+        assert a == sorted(a)                             # one matrix's problems are consecutive
+        for p0, mt, n, z in tiles.tolist():
+            assert n >= 1 and z == 0 and len({rws[p]["a"] for p in range(p0, p0 + n)}) == 1
+            for p in range(p0, p0 + n):
+                key = (rws[p]["out"], mt)
+                assert key not in seen
+                seen[key] = 1
+    expect = {(r["out"], m) for r, (M, _, _) in zip(rows[:-1], dims) for m in range(-(-M // 256))}
+    assert set(seen) == expect
+    assert all(5 not in [r["out"] for r in rws] for _, rws, _ in shared)
+
+
+def test_shared_input_fwd_eligibility():
+    rows, dims = _imcol_rows([(0, 432000, 32, 25, 16)])
+    assert H.shared_fwd_ok(rows[0], *dims[0])
+    assert not H.shared_fwd_ok(dict(rows[0], N=65), 432000, 65, 25)            # > 4 column tiles
+    assert not H.shared_fwd_ok(dict(rows[0], C=104), 432000, 16, 100)          # > 3 register-held k steps
+    assert not H.shared_fwd_ok(dict(rows[0], flags=H.GF_ACCUM), 432000, 16, 25)
+    assert not H.shared_fwd_ok(dict(rows[0], _imcol=0), 432000, 16, 25)
+    # a lone problem takes the same kernel (its bits do not depend on who shares its launch)
+    (v, _, _), = H.gemm3_plan(H.MODE_FWD, [dict(rows[0])], dims)
+    assert v == 5111
