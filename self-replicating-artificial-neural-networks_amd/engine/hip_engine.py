@@ -1616,7 +1616,7 @@ class HipPopulationEngine(PopulationEngine):
                         if ic is not None:
                             wg_rows.append(dict(a=dz, b=ic["buf"].data_ptr(), out=gptr(lay.w[n.id]), bias=dbias,
                                                 aux=yv, act=act, H=OH, W=OW, C=ic["K8"], OH=OH, OW=OW, F=F, KH=1, KW=1,
-                                                SH=1, SW=1, M=F, N=K, K=M, flags=vec))
+                                                SH=1, SW=1, M=F, N=K, K=M, flags=vec, _imcol=1))
                             wg_dims.append((F, K, M))
                         else:
                             # dZ = dY * act'(Y) on load; the bias gradient is reduced inside WGRAD

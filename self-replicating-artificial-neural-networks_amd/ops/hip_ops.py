@@ -762,6 +762,35 @@ def shared_fwd_tiles(items) -> tuple:
     return items, np.concatenate(tl).astype(np.int32)
 
 
+def shared_wgrad_order(rows, tiles: np.ndarray) -> np.ndarray:
+    """WGRAD tiles of first layers over one im2col matrix (rows annotated ``_imcol``, the matrix at ``b``): the
+    tiles of all its problems that read the same row range are made consecutive and dispatched to one XCD, so the
+    matrix rows are fetched into that XCD's L2 once for every organism's filter bank instead of once per organism.
+    Tiles are independent (plain stores, per-split slabs or fixed-point atomics), so only the order changes."""
+    if "wshare" in _OFF or len(tiles) == 0:
+        return tiles
+    first, sid = {}, np.full(len(rows), -1, np.int64)
+    for p, r in enumerate(rows):
+        if r.get("_imcol"):
+            sid[p] = first.setdefault(int(r["b"]), p)
+    counts = np.bincount(sid[sid >= 0], minlength=len(rows)) if (sid >= 0).any() else np.zeros(len(rows), int)
+    shared = counts[sid.clip(0)] >= 2
+    shared &= sid >= 0
+    ts = shared[tiles[:, 0]]
+    if not ts.any():
+        return tiles
+    rest, sh = tiles[~ts], tiles[ts]
+    k0 = sh[:, 3].astype(np.int64) & 0xffff
+    order = np.lexsort((sh[:, 0], sh[:, 1], sh[:, 2], k0, sid[sh[:, 0]]))
+    sh = sh[order]
+    out = []
+    g0 = sid[sh[:, 0]]
+    for s in np.unique(g0):
+        blk = sh[g0 == s]
+        out.append(xcd_swizzle(blk, int(counts[s])))
+    return np.concatenate([rest] + out).astype(tiles.dtype)
+
+
 TILED_BNS = (64, 128, 160, 192)               # gemm3.hip g3_tiled_kernel instantiations
 
 
@@ -950,6 +979,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
                 rg = DWGRAD_RG if v >= 5000000 else (2 if (v % 1000000) % 1000 >= 500 else 1)
                 tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
+                tiles = shared_wgrad_order([r for r, _ in items], tiles)
                 for (r, (M, N, K)), t_ in zip(items, tg):
                     ns = wgrad_splits(K, t_, min(32, t_))
                     if ns == 1:

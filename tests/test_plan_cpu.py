@@ -331,3 +331,25 @@ def test_shared_input_fwd_eligibility():
     # a lone problem takes the same kernel (its bits do not depend on who shares its launch)
     (v, _, _), = H.gemm3_plan(H.MODE_FWD, [dict(rows[0])], dims)
     assert v == 5111
+
+
+def test_shared_wgrad_order_is_a_permutation_grouping_row_ranges():
+    """First-layer WGRADs over one im2col matrix: the tiles of its problems that reduce the same row range are
+    dispatched to one XCD (its L2 serves the matrix rows to every organism); the table stays a permutation and the
+    other problems' tiles keep their order."""
+    rows = [dict(b=1000, _imcol=1), dict(b=2000, _imcol=1), dict(b=1000, _imcol=1), dict(b=1000, _imcol=1),
+            dict(b=1000, _imcol=0)]
+    tl = []
+    for p in range(len(rows)):
+        for k in range(40):                               # 40 row ranges of 16 k steps, one (m, n) tile
+            tl.append((p, 0, 0, (16 * k) | ((16 * k + 16) << 16)))
+    tiles = np.array(tl, np.int32)
+    out = H.shared_wgrad_order(rows, tiles)
+    assert sorted(map(tuple, out.tolist())) == sorted(map(tuple, tiles.tolist()))
+    pos = {tuple(t): i for i, t in enumerate(out.tolist())}
+    nfull = (3 * 40 // (H.XCDS * 3)) * H.XCDS * 3 // 3      # row ranges inside whole swizzle groups
+    for k in range(nfull):
+        w = (16 * k) | ((16 * k + 16) << 16)
+        assert len({pos[(p, 0, 0, w)] % H.XCDS for p in (0, 2, 3)}) == 1
+    keep = [t for t in out.tolist() if t[0] in (1, 4)]
+    assert keep == [t for t in tiles.tolist() if t[0] in (1, 4)]
