@@ -70,6 +70,14 @@ def test_decomposition_is_per_problem():
     full = _split_signature(H.MODE_FWD, fw, fdims)
     for r, d in zip(fw, fdims):
         assert _split_signature(H.MODE_FWD, [r], [d])[r["out"]] == full[r["out"]]
+    # shared-input first layers: the kernel family (and so the arithmetic of every column) is the same alone as in
+    # a run with other organisms' filter banks
+    rows, dims = _imcol_rows([(0, 432000, 32, 25, 16), (0, 432000, 32, 25, 40), (0, 432000, 32, 25, 8)])
+    fam = lambda v: (5100 < v < 5200, (v // 10) % 10)                        # (shared kernel, k steps)
+    together = {r["out"]: fam(v) for v, rws, _ in H.gemm3_plan(H.MODE_FWD, [dict(r) for r in rows], dims) for r in rws}
+    for r, d in zip(rows, dims):
+        (v, _, _), = H.gemm3_plan(H.MODE_FWD, [dict(r)], [d])
+        assert fam(v) == together[r["out"]] == (True, 1)
     # fused chain and conv+pool: functions of the problem alone
     assert H.gchain_rpb(72000, H.GC_BFULL, 96, 100) == H.gchain_rpb(72000, H.GC_BFULL, 96, 100)
     assert H.convpool_wgrad_imgs(750, 32) == 4 and H.convpool_wgrad_imgs(80, 16) == 4
