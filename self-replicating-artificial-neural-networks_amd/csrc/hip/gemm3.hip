@@ -1136,6 +1136,152 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
 }
 
 // ==================================================================================================
+// WGRAD of a small filter bank over a long reduction (round 6): F <= 16 filters, N <= 16 NK columns, 1x1 stride-1
+// geometry -- the first layers over the shared im2col matrix (F = 8 / 16, N = 9 / 25 / 49 taps, 100k-500k rows) and
+// small Dense layers.  The whole [F x N] output is one 16-row MFMA tile, so g3_wgrad_kernel's 64-row f tile left 3 of
+// its 4 waves on zero rows, every 64-row step behind two block barriers.  Here each wave walks its own 64-row steps
+// (wave w: steps w, w + 4, ... of the block's range) through a wave-private LDS stage (no block barrier in the loop,
+// two register sets: a step's loads are issued two of its steps ahead), and the 4 partial tiles and bias sums meet
+// in LDS in wave order at the end (deterministic); wave 0 flushes them with g3_wgrad_kernel's epilogue (Q40 store,
+// fused Adam, or the split's fp32 slab).
+template <int NK>
+__global__ __launch_bounds__(256) void g3_wgrad_tiny_kernel(const GemmDesc* __restrict__ descs,
+                                                            const int4* __restrict__ tiles) {
+    constexpr int BKM = 64, BNK = 16 * NK, AS = BKM * 16, BS = BKM * BNK, BCH = 2 * NK;
+    __shared__ __attribute__((aligned(16))) bf16_t smem[4 * (AS + BS)];
+    const int4 td = tiles[blockIdx.x];
+    const GemmDesc& d = descs[td.x];
+    const G3 g = geo3(d);                 // M = F (<= 16), N (<= BNK) columns, K rows; X row m = im2col row m
+    const int kt0 = td.w & 0xffff, kt1 = (td.w >> 16) & 0xffff;   // 32-row units
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    bf16_t* __restrict__ As = smem + wave * (AS + BS);
+    bf16_t* __restrict__ Bs = As + AS;
+    const int mlim = min(g.K, kt1 * 32);
+    const rsrc_t rZ = mkrsrc(d.a, (int64_t)g.K * g.F * 2);
+    const rsrc_t rY = mkrsrc(d.aux, d.aux ? (int64_t)g.K * g.F * 2 : 0);
+    const rsrc_t rX = mkrsrc(d.b, (int64_t)g.K * g.C * 2);
+    long long* __restrict__ dbias = reinterpret_cast<long long*>(d.bias);
+    // A (dZ, Y): chunk c = lane + 64 p -> row c / 2, filters (c % 2) * 8 .. + 7 (a lane keeps one filter group)
+    const int a_f = (lane & 1) * 8, a_nv = min(8, g.F - a_f);
+    // B (X): chunk c = lane + 64 p -> row c / BCH, columns (c % BCH) * 8 .. + 7
+    int aoff[2], arow[2], boff[BCH], brow[BCH];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int c = lane + 64 * p;
+        arow[p] = a_nv > 0 ? (c >> 1) : (1 << 30);
+        aoff[p] = ((c >> 1) * g.F + a_f) * 2;
+    }
+#pragma unroll
+    for (int p = 0; p < BCH; ++p) {
+        const int c = lane + 64 * p, col = (c % BCH) * 8;
+        brow[p] = col < g.N ? c / BCH : (1 << 30);
+        boff[p] = ((c / BCH) * g.C + col) * 2;
+    }
+    const int nst = (kt1 - kt0 + 1) >> 1;             // 64-row steps of the block
+    Frag ra0[2], ry0[2], rb0[BCH], ra1[2], ry1[2], rb1[BCH];
+    auto load = [&](int s, Frag (&ra)[2], Frag (&ry)[2], Frag (&rb)[BCH]) {
+        const int m0 = (kt0 + 2 * s) * 32, lim = mlim - m0;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int off = arow[p] < lim ? aoff[p] + m0 * g.F * 2 : OOB;
+            ra[p].u = bl16b(rZ, off);
+            if (g.act != ACT_LINEAR) ry[p].u = bl16b(rY, off);
+        }
+#pragma unroll
+        for (int p = 0; p < BCH; ++p) rb[p].u = bl16b(rX, brow[p] < lim ? boff[p] + m0 * g.C * 2 : OOB);
+    };
+    float bsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+    auto stash = [&](Frag (&ra)[2], const Frag (&ry)[2], const Frag (&rb)[BCH]) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            uint4 v = ra[p].u;
+            if (g.act != ACT_LINEAR) v = mul_act_grad(v, ry[p].u, g.act);
+            if (a_nv < 8) v = splice(v, make_uint4(0, 0, 0, 0), a_nv);
+            Frag f;
+            f.u = v;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += bf2f(f.h[j]);
+            *reinterpret_cast<uint4*>(&As[tr_swz<1>((lane + 64 * p) >> 1, a_f)]) = v;
+        }
+#pragma unroll
+        for (int p = 0; p < BCH; ++p) {
+            const int c = lane + 64 * p;
+            *reinterpret_cast<uint4*>(&Bs[tr_swz<NK>(c / BCH, (c % BCH) * 8)]) = rb[p].u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    f32x4_t acc[1][NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) acc[0][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    auto compute = [&]() {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int mr = sub * 32 + grp * 8 + q;
+            const bf16x8_t fa = tr_frag(&As[tr_swz<1>(mr, 4 * pp)], &As[tr_swz<1>(mr + 4, 4 * pp)]);
+#pragma unroll
+            for (int j = 0; j < NK; ++j) {
+                const int col = j * 16 + 4 * pp;
+                const bf16x8_t fb = tr_frag(&Bs[tr_swz<NK>(mr, col)], &Bs[tr_swz<NK>(mr + 4, col)]);
+                acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[0][j], 0, 0, 0);
+            }
+        }
+    };
+    if (wave < nst) load(wave, ra0, ry0, rb0);
+    if (wave + 4 < nst) load(wave + 4, ra1, ry1, rb1);
+    for (int s = wave; s < nst; s += 8) {
+        stash(ra0, ry0, rb0);
+        if (s + 8 < nst) load(s + 8, ra0, ry0, rb0);
+        compute();
+        if (s + 4 >= nst) break;
+        stash(ra1, ry1, rb1);
+        if (s + 12 < nst) load(s + 12, ra1, ry1, rb1);
+        compute();
+    }
+    // bias partials: lanes of one filter group differ in bits 1..5
+#pragma unroll
+    for (int xo = 2; xo < 64; xo <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += __shfl_xor(bsum[j], xo, 64);
+    // the waves' tiles and bias sums meet in LDS (the stages are dead), summed by wave 0 in wave order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    constexpr int PER = NK * 4 + 8;
+    static_assert(3 * PER * 64 * 4 <= 4 * (AS + BS) * 2, "wave reduction must fit in the stages");
+    if (wave > 0) {
+#pragma unroll
+        for (int j = 0; j < NK; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[((wave - 1) * PER + j * 4 + r) * 64 + lane] = acc[0][j][r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[((wave - 1) * PER + NK * 4 + j) * 64 + lane] = bsum[j];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+#pragma unroll
+        for (int j = 0; j < NK; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[0][j][r] += red[(w * PER + j * 4 + r) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += red[(w * PER + NK * 4 + j) * 64 + lane];
+    }
+    if (dbias != nullptr && lane < 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < a_nv) fx_add(dbias + a_f + j, bsum[j]);
+    }
+    float* slab = (d.flags & GF_WSLAB) ? reinterpret_cast<float*>(d.ext) + (int64_t)(kt0 / (int)d.kper) * g.M * g.N
+                                       : nullptr;
+    wgrad_flush<1, NK>(d, g, acc, 0, 0, lane, nullptr, 0, slab);
+}
+
+// ==================================================================================================
 // Dense / 1x1 stride-1 WGRAD with an LDS-DMA staging ring (round 5).  Same tiles, splits and flush as
 // g3_wgrad_kernel, but the dY (and Y) and X row panels of a 64-row step go global -> LDS by buffer_load ... lds
 // (no VGPR staging, no ds_write): each lane of a wave instruction fetches the 16-B piece the XOR-swizzled
@@ -2816,6 +2962,17 @@ bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_
 // part 0: Dense / 1x1 and narrow WGRAD
 bool gemm3_launch_part0(int mode, int variant, dim3 grid, dim3 block, hipStream_t s, const GemmDesc* dp,
                           const int4* tp) {
+    if (mode == MODE_WGRAD && variant > 8000000 && variant < 8000010) {
+        // small-bank WGRAD (F <= 16, N <= 16 NK): 8000000 + NK
+        switch (variant - 8000000) {
+            case 1: hipLaunchKernelGGL((g3_wgrad_tiny_kernel<1>), grid, block, 0, s, dp, tp); break;
+            case 2: hipLaunchKernelGGL((g3_wgrad_tiny_kernel<2>), grid, block, 0, s, dp, tp); break;
+            case 4: hipLaunchKernelGGL((g3_wgrad_tiny_kernel<4>), grid, block, 0, s, dp, tp); break;
+            default: throw std::runtime_error("gemm3: unknown small-bank WGRAD variant " + std::to_string(variant));
+        }
+        SERANN_CHECK(hipGetLastError());
+        return true;
+    }
     if (mode == MODE_WGRAD && variant >= 5000000) {
         // LDS-DMA Dense / 1x1 WGRAD: 5000000 + BMF * 1000 + BNK (+ 500: act' from a staged Y tile)
         const int v = variant - 5000000;

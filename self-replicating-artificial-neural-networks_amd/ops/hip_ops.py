@@ -570,6 +570,8 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
 def gemm3_block(mode: int, variant: int):
     """(rows, cols) of the output tile one block of a v3 launch covers."""
     if mode == MODE_WGRAD:
+        if 8000000 < variant < 8000010:
+            return (16, 16 * (variant - 8000000))      # small-bank WGRAD: the whole [F x N] tile
         v = variant % 1000000
         return (v // 1000, (v % 1000) % 500)
     if mode == MODE_FWD and 5100 < variant < 5200:
@@ -762,6 +764,15 @@ def shared_fwd_tiles(items) -> tuple:
     return items, np.concatenate(tl).astype(np.int32)
 
 
+def tiny_wgrad_ok(r: dict, M: int, N: int, K: int) -> bool:
+    """WGRAD row for g3_wgrad_tiny_kernel: a 1x1 stride-1 problem whose whole [F x N] output is one 16-row MFMA
+    tile of at most 4 column tiles (F <= 16, N <= 64) over a reduction long enough to split (>= 64 k steps: the
+    first layers over the shared im2col matrix); a function of the problem alone."""
+    if "tiny" in _OFF or M > 16 or N > 64 or -(-K // BK) < 64:
+        return False
+    return all(int(r.get(k, 1)) == 1 for k in ("KH", "KW", "SH", "SW"))
+
+
 def shared_wgrad_order(rows, tiles: np.ndarray) -> np.ndarray:
     """WGRAD tiles of first layers over one im2col matrix (rows annotated ``_imcol``, the matrix at ``b``): the
     tiles of all its problems that read the same row range are made consecutive and dispatched to one XCD, so the
@@ -885,6 +896,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             cfg = conv_wgrad_config(r, M)
             if cfg is not None:
                 v = 3000000 + 100000 * cfg[2] + cfg[0] * 1000 + cfg[1] // 64   # (BNK / 64: column tiles per wave)
+        if mode == MODE_WGRAD and v is None and tiny_wgrad_ok(r, M, N, K):
+            v = 8000000 + (1 if N <= 16 else (2 if N <= 32 else 4))     # small-bank WGRAD (g3_wgrad_tiny_kernel)
         if v is None:
             v = gemm3_variant(mode, M, N, K, r)
             if mode == MODE_WGRAD and WGRAD_WIDE and 64 < M <= 192 and N > 16 and v < 1000000 \
@@ -976,7 +989,7 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             bm, bn = gemm3_block(mode, v)
             dms = [dm for _, dm in items]
             if mode == MODE_WGRAD:
-                rg = DWGRAD_RG if v >= 5000000 else (2 if (v % 1000000) % 1000 >= 500 else 1)
+                rg = 1 if v >= 8000000 else (DWGRAD_RG if v >= 5000000 else (2 if (v % 1000000) % 1000 >= 500 else 1))
                 tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 tiles = shared_wgrad_order([r for r, _ in items], tiles)

@@ -114,6 +114,9 @@ SHAPES = [  # B, H, W, C, F, KH, KW, SH, SW, act
     (5, 24, 24, 32, 16, 7, 7, 1, 1, "linear"),
     (4, 14, 14, 61, 64, 5, 5, 1, 1, "relu"),
     (3, 24, 24, 16, 16, 5, 5, 2, 2, "sigmoid"),
+    # small-bank WGRAD (F <= 16, <= 64 columns, 1x1): one MFMA row tile per block, waves on their own row steps
+    (10, 26, 26, 9, 16, 1, 1, 1, 1, "relu"),
+    (12, 20, 20, 49, 8, 1, 1, 1, 1, "linear"),
     # production-batch first layers on a one-channel input (RT = 4 DGRAD into C = 1)
     (750, 28, 28, 1, 32, 7, 7, 1, 1, "linear"),
     (48, 32, 16, 1, 32, 5, 5, 1, 1, "linear"),
@@ -390,7 +393,10 @@ def test_loss_kernel_matches_keras_losses():
     assert abs(m[2].item() / B - mse.item()) < 1e-5
 
 
-@pytest.mark.parametrize("shape", [(3, 9, 9, 8, 13, 3, 3), (3, 9, 9, 2, 13, 1, 1), (50, 12, 12, 1, 70, 1, 1)])
+@pytest.mark.parametrize("shape", [(3, 9, 9, 8, 13, 3, 3), (3, 9, 9, 2, 13, 1, 1), (50, 12, 12, 1, 70, 1, 1),
+                                   # small-bank WGRAD (g3_wgrad_tiny_kernel: F <= 16, N = 9 / 25 / 49 columns, as the
+                                   # first layers over an im2col matrix), odd row widths and F = 13
+                                   (40, 16, 16, 9, 16, 1, 1), (30, 14, 14, 25, 13, 1, 1), (20, 20, 20, 49, 8, 1, 1)])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
 def test_fused_act_grad_and_bias_grad(act, shape):
     """WGRAD/DGRAD apply dZ = dY * act'(Y) on load; WGRAD also reduces the bias gradient

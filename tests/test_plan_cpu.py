@@ -361,3 +361,25 @@ def test_shared_wgrad_order_is_a_permutation_grouping_row_ranges():
         assert len({pos[(p, 0, 0, w)] % H.XCDS for p in (0, 2, 3)}) == 1
     keep = [t for t in out.tolist() if t[0] in (1, 4)]
     assert keep == [t for t in tiles.tolist() if t[0] in (1, 4)]
+
+
+def test_small_bank_wgrad_selection():
+    """g3_wgrad_tiny_kernel takes 1x1 WGRADs of <= 16 filters and <= 64 columns over >= 64 k steps (8000000 + NK),
+    with one row group; conv geometries, wide banks and short reductions keep the other kernels."""
+    geo = dict(H=26, W=26, OH=26, OW=26, KH=1, KW=1, SH=1, SW=1, flags=0)
+    cases = [((16, 9, 507000), 8000001), ((8, 25, 432000), 8000002), ((13, 49, 300000), 8000004),
+             ((32, 9, 507000), None), ((16, 81, 300000), None), ((16, 9, 750), None)]
+    for (M, N, K), want in cases:
+        r = dict(a=1, b=2, out=3, M=M, N=N, K=K, C=N, F=M, **geo)
+        (v, rws, tiles), = H.gemm3_plan(H.MODE_WGRAD, [r], [(M, N, K)])
+        if want is None:
+            assert not 8000000 < v < 8000010
+        else:
+            assert v == want and H.gemm3_block(H.MODE_WGRAD, v) == (16, 16 * (want - 8000000))
+            assert (tiles[:, 1] == 0).all() and (tiles[:, 2] == 0).all()
+            spans = sorted((t & 0xffff, t >> 16) for t in tiles[:, 3].tolist())
+            assert spans[0][0] == 0 and spans[-1][1] == -(-K // H.BK)
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))          # the k ranges tile the reduction
+    r = dict(a=1, b=2, out=3, M=16, N=9, K=507000, C=9, F=16, **dict(geo, KH=3, KW=3))
+    (v, _, _), = H.gemm3_plan(H.MODE_WGRAD, [r], [(16, 81, 507000)])
+    assert not 8000000 < v < 8000010
