@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(64 * NWV * RG) WG_OCC void g3_wgrad_kernel(const Ge
 // in LDS in wave order at the end (deterministic); wave 0 flushes them with g3_wgrad_kernel's epilogue (Q40 store,
 // fused Adam, or the split's fp32 slab).
 template <int NK>
-__global__ __launch_bounds__(256) void g3_wgrad_tiny_kernel(const GemmDesc* __restrict__ descs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NK == 1 ? 4 : (NK == 2 ? 3 : 2)))) void g3_wgrad_tiny_kernel(const GemmDesc* __restrict__ descs,
                                                             const int4* __restrict__ tiles) {
     constexpr int BKM = 64, BNK = 16 * NK, AS = BKM * 16, BS = BKM * BNK, BCH = 2 * NK;
     __shared__ __attribute__((aligned(16))) bf16_t smem[4 * (AS + BS)];
@@ -1164,31 +1164,24 @@ __global__ __launch_bounds__(256) void g3_wgrad_tiny_kernel(const GemmDesc* __re
     // A (dZ, Y): chunk c = lane + 64 p -> row c / 2, filters (c % 2) * 8 .. + 7 (a lane keeps one filter group)
     const int a_f = (lane & 1) * 8, a_nv = min(8, g.F - a_f);
     // B (X): chunk c = lane + 64 p -> row c / BCH, columns (c % BCH) * 8 .. + 7
-    int aoff[2], arow[2], boff[BCH], brow[BCH];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const int c = lane + 64 * p;
-        arow[p] = a_nv > 0 ? (c >> 1) : (1 << 30);
-        aoff[p] = ((c >> 1) * g.F + a_f) * 2;
-    }
-#pragma unroll
-    for (int p = 0; p < BCH; ++p) {
-        const int c = lane + 64 * p, col = (c % BCH) * 8;
-        brow[p] = col < g.N ? c / BCH : (1 << 30);
-        boff[p] = ((c / BCH) * g.C + col) * 2;
-    }
+    // (chunk p of a lane is its chunk 0 moved down 32 / (64 / BCH) rows: one offset and one row key per operand)
+    const int arow = a_nv > 0 ? (lane >> 1) : (1 << 30), aoff = ((lane >> 1) * g.F + a_f) * 2;
+    const int bcol = (lane % BCH) * 8;
+    const int brow = bcol < g.N ? lane / BCH : (1 << 30), boff = ((lane / BCH) * g.C + bcol) * 2;
+    constexpr int BRP = 64 / BCH;                     // rows between a lane's B chunks
     const int nst = (kt1 - kt0 + 1) >> 1;             // 64-row steps of the block
     Frag ra0[2], ry0[2], rb0[BCH], ra1[2], ry1[2], rb1[BCH];
     auto load = [&](int s, Frag (&ra)[2], Frag (&ry)[2], Frag (&rb)[BCH]) {
         const int m0 = (kt0 + 2 * s) * 32, lim = mlim - m0;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            const int off = arow[p] < lim ? aoff[p] + m0 * g.F * 2 : OOB;
+            const int off = arow + 32 * p < lim ? aoff + (m0 + 32 * p) * g.F * 2 : OOB;
             ra[p].u = bl16b(rZ, off);
             if (g.act != ACT_LINEAR) ry[p].u = bl16b(rY, off);
         }
 #pragma unroll
-        for (int p = 0; p < BCH; ++p) rb[p].u = bl16b(rX, brow[p] < lim ? boff[p] + m0 * g.C * 2 : OOB);
+        for (int p = 0; p < BCH; ++p)
+            rb[p].u = bl16b(rX, brow + BRP * p < lim ? boff + (m0 + BRP * p) * g.C * 2 : OOB);
     };
     float bsum[8];
 #pragma unroll
