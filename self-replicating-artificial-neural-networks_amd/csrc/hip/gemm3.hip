@@ -3129,32 +3129,40 @@ void g3_shared_fwd_kernel(const GemmDesc* __restrict__ descs, const int4* __rest
             fa[s][i].u = bl16(rA, (row < M && k < C) ? row * C + k : -1);
         }
     const int nrows = min(WROWS, M - m_w);
-    for (int q = 0; q < nprob; ++q) {
-        const GemmDesc& d = descs[td.x + q];
-        const int N = (int)d.N, K = (int)d.K, act = (int)d.act, flags = (int)d.flags;
+    // a problem's filter bank: loaded while the previous problem's tile is being stored (one bank in flight)
+    auto load_bank = [&](const GemmDesc& d, Frag (&fb)[KS][NT]) {
+        const int N = (int)d.N, K = (int)d.K;
         const rsrc_t rB = mkrsrc(d.b, (int64_t)N * K * 2);
         const int brow = min(r16, N - 1) * K;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int k = s * 32 + kg;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = j * 16 + r16;
+                fb[s][j].u = bl16(rB, (k < K && n < N) ? brow + j * 16 * K + k : -1);
+                if (k + 8 > K) fb[s][j].u = splice(fb[s][j].u, make_uint4(0, 0, 0, 0), K - k);
+            }
+        }
+    };
+    Frag fb[KS][NT];
+    load_bank(d0, fb);
+    for (int q = 0; q < nprob; ++q) {
+        const GemmDesc& d = descs[td.x + q];
+        const int N = (int)d.N, act = (int)d.act, flags = (int)d.flags;
         f32x4_t acc[RT][NT];
 #pragma unroll
         for (int i = 0; i < RT; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int k = s * 32 + kg;
-            Frag fb[NT];
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const int n = j * 16 + r16;
-                fb[j].u = bl16(rB, (k < K && n < N) ? brow + j * 16 * K + k : -1);
-                if (k + 8 > K) fb[j].u = splice(fb[j].u, make_uint4(0, 0, 0, 0), K - k);
-            }
+        for (int s = 0; s < KS; ++s)
 #pragma unroll
             for (int i = 0; i < RT; ++i)
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i].v, fb[j].v, acc[i][j], 0, 0, 0);
-        }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i].v, fb[s][j].v, acc[i][j], 0, 0, 0);
+        if (q + 1 < nprob) load_bank(descs[td.x + q + 1], fb);
         const float* bias = reinterpret_cast<const float*>(d.bias);
         if (flags & GF_BNUSTAT) {
             bn_ustat_flush<RT, NT, 1>(d, acc, [&](int i, int rr) { return m_w + i * 16 + rr < M; }, 0, N, bias, act,
