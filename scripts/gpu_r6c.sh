@@ -56,4 +56,13 @@ if has anat; then
   done
 fi
 has bench && step bench 900 python bench.py --steps ${BSTEPS:-3} --warmup 1
+# smoke: the driver's smoke() on this tree;  bench20: the driver's 1-GPU bench command (20 timed generations after 5)
+has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+has bench20 && step bench20 900 python bench.py --steps 20 --warmup 5
+if has prof; then
+  rm -rf gpurun_out/r6c/prof
+  step prof 500 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r6c/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1
+  f=$(find gpurun_out/r6c/prof -name "*kernel_stats.csv" | head -1); cp "$f" gpurun_out/r6c/bench_kernel_stats.csv
+  rm -rf gpurun_out/r6c/prof
+fi
 exit 0
