@@ -538,6 +538,10 @@ IMCOL_ROWS = 64
 TRANS_ELEMS = 4096
 
 
+# rows per wave (16-row tiles) of the direct-fragment DGRAD onto <= 16 channels (instantiated: 2, 4)
+DGRAD_NT1_RT = int(_os.environ.get("SERANN_DGRAD_NT1_RT", "4"))
+
+
 def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
     """Kernel instantiation of the v3 kernels (gemm3.hip launch_gemm3 encoding) for one problem.
 
@@ -564,6 +568,8 @@ def gemm3_variant(mode: int, M: int, N: int, K: int, geo: dict) -> int:
         return 5000 + nt + 10 * (2 if nt == 8 else 4)
     kw = M <= 8192 and -(-K // BK) >= 16
     rt = 2 if (kw or nt == 8 or M < 16384) else 4
+    if mode == MODE_DGRAD and nt == 1 and rt == 4:
+        rt = DGRAD_NT1_RT                  # conv DGRAD onto <= 16 channels (A/B knob)
     return nt + 10 * rt + (100 if kw else 0) + (1000 if gen else 0)
 
 
