@@ -3230,6 +3230,7 @@ bool gemm3_launch_part3(int mode, int variant, dim3 grid, dim3 block, hipStream_
     D3(MODE_, 1, 2, true) D3(MODE_, 2, 2, true) D3(MODE_, 4, 2, true) D3(MODE_, 8, 2, true)
     D3ALL(MODE_FWD)
     D3ALL(MODE_DGRAD)
+    D3(MODE_DGRAD, 1, 8, false)          // DGRAD onto <= 16 channels, 8 row tiles per wave (hip_ops.DGRAD_NT1_RT)
 #undef D3ALL
 #undef D3
     return false;

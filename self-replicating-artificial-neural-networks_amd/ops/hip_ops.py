@@ -538,7 +538,8 @@ IMCOL_ROWS = 64
 TRANS_ELEMS = 4096
 
 
-# rows per wave (16-row tiles) of the direct-fragment DGRAD onto <= 16 channels (instantiated: 2, 4)
+# rows per wave (16-row tiles) of the direct-fragment DGRAD onto <= 16 channels (instantiated: 2, 4, 8; 2 measured
+# 3 % slower on the generation-15 mix, profiles/r6/ab_dgrad_nt1_rt2_rejected.txt)
 DGRAD_NT1_RT = int(_os.environ.get("SERANN_DGRAD_NT1_RT", "4"))
 
 
