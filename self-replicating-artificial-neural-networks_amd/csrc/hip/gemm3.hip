@@ -302,9 +302,13 @@ __device__ __forceinline__ void wave_store_rows(bf16_t* __restrict__ st, bf16_t*
 }  // namespace
 
 
-// GF_BNUSTAT (FWD epilogues of the conv-halo, direct and LDS-tiled kernels): this output feeds a BatchNormalization
-// -- accumulate its phase-0 statistics here, unshifted (K = 0: sum x and sum x^2 of the stored bf16 values; the BN's
-// flag 512 makes phase 2 finish them in double, where the integer-exact sums lose nothing to cancellation).  A
+// GF_BNUSTAT (FWD epilogues of the conv-halo, direct, LDS-tiled and shared-input kernels): this output feeds a
+// BatchNormalization -- accumulate its phase-0 statistics here, unshifted (K = 0: sum x and sum x^2 of the stored bf16
+// values; the BN's flag 512 makes phase 2 finish them in double).  The per-wave partials are fp32 sums of at most
+// RT * 16 values before they reach the fixed-point workspace, so E[x^2] - mean^2 keeps ~2^-24 relative error of
+// E[x^2]: channels with |mean| >> std lose that much of their variance (tests/test_gpu_kernels.py::
+// test_fwd_epilogue_bn_statistics checks both sums against the stored outputs' at |mean| > std; phase 0's shifted
+// sums remain the path for outputs that do not take this epilogue).  A
 // wave's rows of each accumulator column are summed in fp32 in a fixed order, the waves' partials meet in LDS in
 // wave order, and the block adds them to its stripe of the wide fixed-point workspace d.aux: one atomic pair per
 // column and sum per block (deterministic).  The block's 4 waves cover WG column groups of NT * 16 columns (wave w:
