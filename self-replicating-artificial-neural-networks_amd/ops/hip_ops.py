@@ -771,6 +771,10 @@ def shared_fwd_tiles(items) -> tuple:
     return items, np.concatenate(tl).astype(np.int32)
 
 
+# k steps (32 rows) per small-bank WGRAD block; 0: the Dense WGRAD rule (wgrad_target)
+TINY_WGRAD_TARGET = int(_os.environ.get("SERANN_TINY_WGRAD_TARGET", "0"))
+
+
 def tiny_wgrad_ok(r: dict, M: int, N: int, K: int) -> bool:
     """WGRAD row for g3_wgrad_tiny_kernel: a 1x1 stride-1 problem whose whole [F x N] output is one 16-row MFMA
     tile of at most 4 column tiles (F <= 16, N <= 64) over a reduction long enough to split (>= 64 k steps: the
@@ -998,6 +1002,8 @@ def gemm3_plan(mode: int, rows, dims, splitk: bool = False):
             if mode == MODE_WGRAD:
                 rg = 1 if v >= 8000000 else (DWGRAD_RG if v >= 5000000 else (2 if (v % 1000000) % 1000 >= 500 else 1))
                 tg = [wgrad_target(M, N, K, bm, bn, rg) for (M, N, K) in dms]
+                if 8000000 < v < 8000010 and TINY_WGRAD_TARGET > 0:
+                    tg = [TINY_WGRAD_TARGET] * len(dms)       # k steps per small-bank WGRAD block (A/B knob)
                 tiles = gemm_tiles(dms, mode, target_ksteps=tg, bm=bm, bn=bn, swizzle=True)
                 tiles = shared_wgrad_order([r for r, _ in items], tiles)
                 for (r, (M, N, K)), t_ in zip(items, tg):
